@@ -1,0 +1,167 @@
+// Host-side launch logic for one compiled model configuration (Ops<M>) and
+// the type-erased registry entry the C-ABI (ude_rk4.hip) dispatches on.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include "ude_rk4.h"
+#include "ude_kernels.h"
+
+namespace ude {
+
+template <class M>
+bool matches(const UdeModelDesc* d) {
+  if (d->kind != M::KIND || d->n_regions != M::R || d->latent_dim != M::L) return false;
+  if (M::HAS_P) {
+    if (d->n_p_hidden != M::NPH) return false;
+    for (int i = 0; i < M::NPH; ++i) if (d->p_hidden[i] != M::hid(0, i)) return false;
+  }
+  if (M::HAS_A) {
+    if (d->n_a_hidden != M::NAH) return false;
+    for (int i = 0; i < M::NAH; ++i) if (d->a_hidden[i] != M::hid(1, i)) return false;
+  }
+  return true;
+}
+
+#define HIPCHK(x) do { if ((x) != hipSuccess) return UDE_E_HIP; } while (0)
+
+template <class M>
+struct Ops {
+  static int ensure_attrs() {
+    static bool done = false;
+    if (done) return UDE_OK;
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_B));
+    done = true;
+    return UDE_OK;
+  }
+
+  static int grids(int device, int n_tiles, int* gf, int* gb) {
+    int rc = ensure_attrs();
+    if (rc) return rc;
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    int of = 0, ob = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, (const void*)&ude_fwd_kernel<M, true>, NTHREADS, M::LDS_F));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_bwd_kernel<M>, NTHREADS, M::LDS_B));
+    if (of < 1) of = 1;
+    if (ob < 1) ob = 1;
+    const long mf = (long)cus * of, mb = (long)cus * ob;
+    *gf = (int)(n_tiles < mf ? n_tiles : mf);
+    *gb = (int)(n_tiles < mb ? n_tiles : mb);
+    if (*gf < 1) *gf = 1;
+    if (*gb < 1) *gb = 1;
+    return UDE_OK;
+  }
+
+  static int query(const UdeProblem* p, int device, UdeSizes* o) {
+    if (p->n_traj < 1 || p->n_steps < 0 || p->n_out < 0) return UDE_E_INVALID;
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(device, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    o->pack_bytes = (int64_t)M::PACK_TOTAL * 4;
+    o->sched_bytes = (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
+    o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * M::F * TT * 4;
+    o->stats_slab_bytes = (int64_t)gf * 5 * 8;
+    o->grad_slab_bytes = (int64_t)gb * M::SLAB_TOTAL * 4;
+    o->n_params = M::N_PARAMS;
+    o->grid_fwd = gf;
+    o->grid_bwd = gb;
+    o->lds_fwd = M::LDS_F;
+    o->lds_bwd = M::LDS_B;
+    return UDE_OK;
+  }
+
+  static int pack(const float* const* W, const float* const* b, float* out, hipStream_t s) {
+    PackPtrs P;
+    memset(&P, 0, sizeof(P));
+    int li = 0;
+    for (int net = 0; net < 2; ++net)
+      for (int i = 0; i < M::nl(net); ++i, ++li) {
+        if (!W[li] || !b[li]) return UDE_E_INVALID;
+        P.W[net][i] = W[li];
+        P.b[net][i] = b[li];
+      }
+    int mx = M::WST_SIZE;
+    for (int net = 0; net < 2; ++net) {
+      if (M::wsf_size(net) > mx) mx = M::wsf_size(net);
+      for (int i = 0; i < M::nl(net); ++i) {
+        if (M::wf_size(net, i) > mx) mx = M::wf_size(net, i);
+        if (M::wt_size(net, i) > mx) mx = M::wt_size(net, i);
+        if (M::b_size(net, i) > mx) mx = M::b_size(net, i);
+      }
+    }
+    dim3 grid((mx + 255) / 256, 33);
+    hipLaunchKernelGGL(ude_pack_kernel<M>, grid, dim3(256), 0, s, P, out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  static int forward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
+                     float* latent, float* ckpt, double* stats_slab, float* stats_out, hipStream_t s) {
+    if (!pack || !sched || !y0 || !latent || !stats_slab || !stats_out) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(dev, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
+    a.latent = latent; a.ckpt = ckpt; a.stats_slab = stats_slab;
+    a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
+    a.fa_w = p->fa_w;
+    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    HIPCHK(hipGetLastError());
+    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  static int backward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
+                      const float* ckpt, const float* dlatent, const float* stats_out, const float* dstats,
+                      float* dy0, float* slab, float* dparams, hipStream_t s) {
+    if (!pack || !sched || !y0 || !dlatent || !stats_out || !dstats || !dy0 || !slab || !dparams) return UDE_E_INVALID;
+    if (p->n_steps > 0 && !ckpt) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(dev, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
+    a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.stats_out = stats_out; a.dstats = dstats;
+    a.dy0 = dy0; a.slab = slab;
+    a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
+    a.fa_w = p->fa_w;
+    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::N_PARAMS + 255) / 256), dim3(256), 0, s,
+                       (const float*)slab, gb, dparams);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+};
+
+struct Entry {
+  bool (*match)(const UdeModelDesc*);
+  int (*query)(const UdeProblem*, int, UdeSizes*);
+  int (*pack)(const float* const*, const float* const*, float*, hipStream_t);
+  int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*, float*, hipStream_t);
+  int (*backward)(const UdeProblem*, const float*, const void*, const float*, const float*, const float*,
+                  const float*, const float*, float*, float*, float*, hipStream_t);
+};
+
+template <class M>
+constexpr Entry make_entry() {
+  return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::forward, &Ops<M>::backward};
+}
+
+
+}  // namespace ude

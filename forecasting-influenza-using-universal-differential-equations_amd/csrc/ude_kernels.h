@@ -1,0 +1,866 @@
+// gfx950 kernels for the batched UDE RK4 solve (forward + VJP).
+//
+// Hot path replaced: torchdiffeq.odeint(ode, z, t, method='rk4',
+// options=dict(step_size=h)) at lib/VAE.py:137 with ode in {Fp, Fa, FaFp}
+// (lib/models.py:109-265), and the autograd backward of lib/VAE.py:203.
+//
+// Execution model (one workgroup = 4 waves = one tile of TT=16 trajectories):
+//  * every MLP layer is a small GEMM  out[o][t] = W[o][:] . in[t][:]  on
+//    v_mfma_f32_16x16x4_f32 (exact fp32); the 16 trajectories are the MFMA N
+//    dimension, output rows are split across the 4 waves (row tiles of 16);
+//  * activations live in LDS as one [t][feature] record per trajectory; weights
+//    stream from L2 in a pre-packed fragment order (one 16-B load per lane feeds
+//    4 MFMAs);
+//  * all 4 RK4 stages of every step run inside the launch; the forward saves the
+//    4 stage inputs per step (3R floats each) for the backward, which recomputes
+//    each stage's activations once and back-propagates through the 3/8-rule;
+//  * the parameter gradient dW[o][i] = sum_{t,eval} g[t][o] in[t][i] is another
+//    MFMA GEMM (K = trajectories) whose accumulators stay in each wave's registers
+//    for the whole launch (the wave owns the rows it computed in the forward);
+//    per-workgroup partials are summed by a separate deterministic pass;
+//  * latent dims >= 3 have zero derivative (lib/models.py:144, :249), so they are
+//    per-trajectory constants: their layer-0 contribution W0[:,static].x + b0 is
+//    hoisted once per tile, and their weight gradient uses the per-trajectory sum
+//    of layer-0 output gradients (one GEMM per tile).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <utility>
+#include <type_traits>
+#include "ude_model.h"
+
+namespace ude {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <class Fn, int... I>
+__device__ __forceinline__ void sfor_i(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void sfor(Fn&& f) {
+  sfor_i(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 f4zero() { f4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
+
+struct KArgs {
+  const float* pack;
+  const float* y0;
+  const unsigned char* sched;
+  float* latent;
+  float* ckpt;
+  double* stats_slab;
+  const float* dlatent;
+  const float* stats_out;
+  const float* dstats;
+  float* dy0;
+  float* slab;
+  int n_traj, n_steps, n_out, n_tiles;
+  float fa_w;
+};
+
+struct Sched {
+  const float* dt;
+  const int* out_start;
+  const int* out_j;
+  const int* out_mode;
+  const float* out_slope;
+  __device__ Sched(const unsigned char* base, int n_steps, int n_out) {
+    dt = (const float*)base;
+    out_start = (const int*)(dt + n_steps);
+    out_j = out_start + n_steps + 1;
+    out_mode = out_j + n_out;
+    out_slope = (const float*)(out_mode + n_out);
+  }
+};
+
+// One 16-row tile of  C[o][t] += sum_k A[o][k] * B[t][k]  with K = KP (multiple of 16).
+// A: packed fragments in global memory ([KP/16][64][4] for this tile);
+// B: the per-trajectory LDS record, lane group g reading features [g*KP/4, (g+1)*KP/4).
+template <int KP>
+__device__ __forceinline__ f4 gemm_tile(const float* __restrict__ wp, const float* bp, int lane, f4 acc) {
+  constexpr int KQ = KP / 4;
+  constexpr int NQ = KP / 16;
+  const f4* w = reinterpret_cast<const f4*>(wp) + lane;
+  const float* b = bp + (lane >> 4) * KQ;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const f4 a = w[q * 64];
+    const f4 x = *reinterpret_cast<const f4*>(b + 4 * q);
+    acc = mfma4(a[0], x[0], acc);
+    acc = mfma4(a[1], x[1], acc);
+    acc = mfma4(a[2], x[2], acc);
+    acc = mfma4(a[3], x[3], acc);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : expm1f(x); }
+
+template <class M, int NZ_>
+using C1Arr = f4[NZ_ > 0 ? NZ_ : 1];
+
+// Forward pass of both MLPs for the stage input held in the record's Y slot.
+// Leaves post-activation outputs of every layer in the record (the final
+// layers' raw outputs: P-net pre-|.| rates q, A-net Fa).  Ends on a barrier.
+template <class M, int W, int SR>
+__device__ __forceinline__ void mlp_forward(const float* __restrict__ pack, float* lds,
+                                            const f4* c1, int lane) {
+  const int t = lane & 15, g = lane >> 4;
+  float* rec = lds + t * SR;
+  sfor<M::D>([&](auto dd) {
+    constexpr int d = decltype(dd)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k);
+        constexpr int rt = M::frt(d, k);
+        constexpr int KP = M::kin(net, d);
+        constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
+        f4 acc;
+        if constexpr (d == 0 && M::S > 0) {
+          acc = c1[M::nz_before(W, k)];
+        } else {
+          acc = *reinterpret_cast<const f4*>(pack + M::b_off(net, d) + rt * 16 + g * 4);
+        }
+        acc = gemm_tile<KP>(pack + M::wf_off(net, d) + rt * (KP / 16) * 256, rec + inoff, lane, acc);
+        if constexpr (M::act(net, d)) {
+          acc[0] = elu1(acc[0]); acc[1] = elu1(acc[1]);
+          acc[2] = elu1(acc[2]); acc[3] = elu1(acc[3]);
+        }
+        *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = acc;
+      }
+    });
+    __syncthreads();
+  });
+}
+
+// Static-feature hoist: c1[o][t] = b0[o] + sum_s W0[o][static s] * x_static[t][s].
+template <class M, int W, int SR, int XOFF>
+__device__ __forceinline__ void static_hoist(const float* __restrict__ pack, const float* lds, f4* c1, int lane) {
+  if constexpr (M::S > 0) {
+    const int t = lane & 15, g = lane >> 4;
+    sfor<M::FT(0)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(0, k) == W) {
+        constexpr int net = M::fnet(0, k);
+        constexpr int rt = M::frt(0, k);
+        f4 acc = *reinterpret_cast<const f4*>(pack + M::b_off(net, 0) + rt * 16 + g * 4);
+        acc = gemm_tile<M::S16>(pack + M::wsf_off(net) + rt * (M::S16 / 16) * 256, lds + t * SR + XOFF, lane, acc);
+        c1[M::nz_before(W, k)] = acc;
+      }
+    });
+  }
+}
+
+// Load the tile's static features (latent dims >= 3 of y0) into the record.
+template <class M, int SR, int XOFF>
+__device__ __forceinline__ void load_static(const float* __restrict__ y0, float* lds, int n0, int n_traj) {
+  if constexpr (M::S > 0) {
+    for (int i = threadIdx.x; i < TT * M::S16; i += NTHREADS) {
+      const int t = i / M::S16, s = i - t * M::S16;
+      const int n = n0 + t;
+      float v = 0.f;
+      if (s < M::S && n < n_traj) {
+        const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
+        v = y0[((size_t)n * M::R + r) * M::L + c];
+      }
+      lds[t * SR + XOFF + s] = v;
+    }
+  }
+}
+
+__device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, int stage, int F, int f, int t) {
+  return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ============================================================================
+// Forward solve
+// ============================================================================
+template <class M, bool TRAIN, int W>
+__device__ void fwd_body(const KArgs& A, float* lds) {
+  constexpr int SR = M::SR_F;
+  constexpr int SL = M::SLOTS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
+
+  for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
+  __syncthreads();
+
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
+    float ys[SL][3], k1[SL][3], k2[SL][3], k3[SL][3];
+
+    // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
+    sfor<SL>([&](auto ss) {
+      constexpr int sl = decltype(ss)::value;
+      const int p = tid + sl * NTHREADS;
+      if (p < M::PAIRS) {
+        const int r = p / TT, t = p - r * TT;
+        const int n = n0 + t;
+        const bool valid = n < A.n_traj;
+        const float* src = A.y0 + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          ys[sl][c] = valid ? src[c] : 0.f;
+          lds[t * SR + M::Y_OFF + 3 * r + c] = ys[sl][c];
+          if (TRAIN && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
+        }
+        if (valid) {
+          float* dst = A.latent + ((size_t)n * M::R + r) * M::L;
+          for (int c = 0; c < M::L; ++c) dst[c] = src[c];
+        }
+      }
+    });
+    load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
+    __syncthreads();
+    f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
+    static_hoist<M, W, SR, M::XSF_OFF>(A.pack, lds, c1, lane);
+    __syncthreads();
+
+    for (int step = 0; step < A.n_steps; ++step) {
+      const float dt = sc.dt[step];
+      for (int j = 0; j < 4; ++j) {
+        mlp_forward<M, W, SR>(A.pack, lds, c1, lane);
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          if (p < M::PAIRS) {
+            const int r = p / TT, t = p - r * TT;
+            const int n = n0 + t;
+            const bool valid = n < A.n_traj;
+            float* rec = lds + t * SR;
+            float Y[3], f[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Y[c] = rec[M::Y_OFF + 3 * r + c];
+            if constexpr (M::HAS_P) {
+              const float q0 = rec[M::act_off(0, M::nl(0) - 1) + 2 * r];
+              const float q1 = rec[M::act_off(0, M::nl(0) - 1) + 2 * r + 1];
+              const float b = fabsf(q0), gm = fabsf(q1);
+              const float plus = (b * Y[0]) * Y[1];
+              const float minus = gm * Y[1];
+              f[0] = -plus; f[1] = plus - minus; f[2] = minus;
+              if (valid) {
+                st_b += (double)b; st_g += (double)gm;
+                st_bb += (double)b * (double)b; st_gg += (double)gm * (double)gm;
+              }
+            }
+            if constexpr (M::HAS_A) {
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                const float fa = rec[M::act_off(1, M::nl(1) - 1) + 3 * r + c];
+                if constexpr (M::HAS_P) f[c] = f[c] + A.fa_w * fa;
+                else f[c] = fa;
+                if (valid) st_fa += (double)fa * (double)fa;
+              }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) f[c] = (Y[c] > 2.f || Y[c] < -1.f) ? 0.f : f[c];
+            float Yn[3];
+            if (j == 0) {
+#pragma unroll
+              for (int c = 0; c < 3; ++c) { k1[sl][c] = f[c]; Yn[c] = ys[sl][c] + (dt * f[c]) * (1.0f / 3.0f); }
+            } else if (j == 1) {
+#pragma unroll
+              for (int c = 0; c < 3; ++c) { k2[sl][c] = f[c]; Yn[c] = ys[sl][c] + dt * (f[c] - k1[sl][c] * (1.0f / 3.0f)); }
+            } else if (j == 2) {
+#pragma unroll
+              for (int c = 0; c < 3; ++c) { k3[sl][c] = f[c]; Yn[c] = ys[sl][c] + dt * ((k1[sl][c] - k2[sl][c]) + f[c]); }
+            } else {
+              float yold[3];
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                yold[c] = ys[sl][c];
+                const float dy = (((k1[sl][c] + 3.0f * (k2[sl][c] + k3[sl][c])) + f[c]) * dt) * 0.125f;
+                ys[sl][c] = ys[sl][c] + dy;
+                Yn[c] = ys[sl][c];
+              }
+              if (valid) {
+                const int o_end = sc.out_start[step + 1];
+                for (int o = sc.out_start[step]; o < o_end; ++o) {
+                  const int jo = sc.out_j[o], mode = sc.out_mode[o];
+                  const float slope = sc.out_slope[o];
+                  float* dst = A.latent + (size_t)jo * NRL + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+                  for (int c = 0; c < 3; ++c) {
+                    float v;
+                    if (mode == 0) v = yold[c];
+                    else if (mode == 1) v = ys[sl][c];
+                    else v = yold[c] + slope * (ys[sl][c] - yold[c]);
+                    dst[c] = v;
+                  }
+                  const float* src = A.y0 + ((size_t)n * M::R + r) * M::L;
+                  for (int c = 3; c < M::L; ++c) dst[c] = src[c];
+                }
+              }
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) rec[M::Y_OFF + 3 * r + c] = Yn[c];
+            if (TRAIN) {
+              const int ns = j == 3 ? step + 1 : step;
+              const int nj = j == 3 ? 0 : j + 1;
+              if (ns < A.n_steps) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                  A.ckpt[ckpt_index(tile, A.n_steps, ns, nj, M::F, 3 * r + c, t)] = Yn[c];
+              }
+            }
+          }
+        });
+        __syncthreads();
+      }
+    }
+  }
+
+  // deterministic per-workgroup partial sums
+  double* red = reinterpret_cast<double*>(lds);
+  double v[5] = {wave_sum(st_b), wave_sum(st_g), wave_sum(st_bb), wave_sum(st_gg), wave_sum(st_fa)};
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) red[(tid >> 6) * 5 + c] = v[c];
+  }
+  __syncthreads();
+  if (tid < 5) {
+    double s = 0;
+    for (int w = 0; w < WAVES; ++w) s += red[w * 5 + tid];
+    A.stats_slab[(size_t)blockIdx.x * 5 + tid] = s;
+  }
+}
+
+template <class M, bool TRAIN>
+__global__ __launch_bounds__(NTHREADS) void ude_fwd_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w == 0) fwd_body<M, TRAIN, 0>(a, lds);
+  else if (w == 1) fwd_body<M, TRAIN, 1>(a, lds);
+  else if (w == 2) fwd_body<M, TRAIN, 2>(a, lds);
+  else fwd_body<M, TRAIN, 3>(a, lds);
+}
+
+// ============================================================================
+// Backward (VJP)
+// ============================================================================
+template <class M, int W, int SR, class DW, class GA, class G0>
+__device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, float* lds,
+                                             DW& dw, GA& gacc, G0& g0t, int lane) {
+  const int t = lane & 15, g = lane >> 4;
+  float* rec = lds + t * SR;
+  sfor<M::D>([&](auto ee) {
+    constexpr int d = M::D - 1 - decltype(ee)::value;
+    // (1) rows owned by this wave: bias/G sums and the dW GEMM (K = trajectories)
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k);
+        constexpr int rt = M::frt(d, k);
+        constexpr int goff = M::gbuf(net, d);
+        constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
+        const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
+        if constexpr (d == 0) g0t[M::nz_before(W, k)] += gv;
+        else gacc[M::ng_before(W, d, k)] += gv;
+        float ga[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
+        sfor<M::rti(net, d)>([&](auto cc) {
+          constexpr int ct = decltype(cc)::value;
+          constexpr int idx = M::ndw_before(W, d, k) + ct;
+          f4 acc = dw[idx];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma4(ga[s], lds[(4 * g + s) * SR + inoff + ct * 16 + t], acc);
+          dw[idx] = acc;
+        });
+      }
+    });
+    // (2) gradient w.r.t. the layer input (rows = input features)
+    sfor<M::XT(d)>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      if constexpr (M::xowner(d, m) == W) {
+        if constexpr (d == 0) {
+          f4 acc = f4zero();
+          if constexpr (M::HAS_P)
+            acc = gemm_tile<M::kout(0, 0)>(pack + M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256,
+                                           rec + M::gbuf(0, 0), lane, acc);
+          if constexpr (M::HAS_A)
+            acc = gemm_tile<M::kout(1, 0)>(pack + M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256,
+                                           rec + M::gbuf(1, 0), lane, acc);
+          *reinterpret_cast<f4*>(rec + M::GY_OFF + m * 16 + g * 4) = acc;
+        } else {
+          constexpr int net = M::xnet(d, m);
+          constexpr int rt = M::xrt(d, m);
+          f4 acc = gemm_tile<M::kout(net, d)>(pack + M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256,
+                                              rec + M::gbuf(net, d), lane, f4zero());
+          if constexpr (M::act(net, d - 1)) {
+            const f4 av = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] = av[e] <= 0.f ? acc[e] * (av[e] + 1.f) : acc[e];
+          }
+          *reinterpret_cast<f4*>(rec + M::gbuf(net, d - 1) + rt * 16 + g * 4) = acc;
+        }
+      }
+    });
+    __syncthreads();
+  });
+}
+
+template <class M, int W>
+__device__ void bwd_body(const KArgs& A, float* lds) {
+  constexpr int SR = M::SR_B;
+  constexpr int SL = M::SLOTS;
+  constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
+  constexpr int NGn = M::NG(W) > 0 ? M::NG(W) : 1;
+  constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int t16 = lane & 15, g = lane >> 4;
+  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_TOTAL;
+
+  // side-statistic cotangents -> per-eval gradient coefficients
+  //   d mean_c / d p = 1/n ;  d std_c / d p = (p - mean_c) / ((n - 1) std_c)   (torch std backward)
+  //   d |Fa| / d Fa = Fa / |Fa|  (0 when |Fa| == 0, torch norm backward)
+  const double nev = 4.0 * (double)A.n_steps * (double)A.n_traj * (double)M::R;
+  float ca[2] = {0.f, 0.f}, cb[2] = {0.f, 0.f}, mu[2] = {0.f, 0.f}, cn = 0.f;
+  if constexpr (M::HAS_P) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      mu[c] = A.stats_out[c];
+      ca[c] = (float)((double)A.dstats[c] / nev);
+      const double sd = (double)A.stats_out[2 + c];
+      cb[c] = (float)((double)A.dstats[2 + c] / ((nev - 1.0) * sd));
+    }
+  }
+  if constexpr (M::HAS_A) {
+    const float nrm = A.stats_out[4];
+    cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
+  }
+
+  f4 dw[NDWn], gacc[NGn], g0t[NZn], c1[NZn];
+#pragma unroll
+  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+#pragma unroll
+  for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
+
+  for (int i = tid; i < M::SLAB_DB - M::SLAB_STATIC; i += NTHREADS) myslab[M::SLAB_STATIC + i] = 0.f;
+  for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
+  __syncthreads();
+
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
+    load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    __syncthreads();
+    static_hoist<M, W, SR, M::XSB_OFF>(A.pack, lds, c1, lane);
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    __syncthreads();
+
+    float a[SL][3];
+#pragma unroll
+    for (int sl = 0; sl < SL; ++sl) a[sl][0] = a[sl][1] = a[sl][2] = 0.f;
+
+    for (int step = A.n_steps - 1; step >= 0; --step) {
+      const float dt = sc.dt[step];
+      float pend[SL][3], accy[SL][3], sdk[SL][3], dk1[SL][3], dk2[SL][3], dk3[SL][3], dyf[SL][2];
+      sfor<SL>([&](auto ss) {
+        constexpr int sl = decltype(ss)::value;
+        const int p = tid + sl * NTHREADS;
+        pend[sl][0] = pend[sl][1] = pend[sl][2] = 0.f;
+        if (p < M::PAIRS) {
+          const int r = p / TT, t = p - r * TT;
+          const int n = n0 + t;
+          if (n < A.n_traj) {
+            const int o_end = sc.out_start[step + 1];
+            for (int o = sc.out_start[step]; o < o_end; ++o) {
+              const int jo = sc.out_j[o], mode = sc.out_mode[o];
+              const float slope = sc.out_slope[o];
+              const float* gl = A.dlatent + (size_t)jo * NRL + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                // y1-side / y0-side shares of d latent[jo] (torchdiffeq _linear_interp)
+                const float gv = gl[c];
+                const float sg = mode == 2 ? slope * gv : (mode == 1 ? gv : 0.f);
+                const float pg = mode == 2 ? gv - sg : (mode == 0 ? gv : 0.f);
+                a[sl][c] += sg;
+                pend[sl][c] += pg;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float s = (a[sl][c] * 0.125f) * dt;
+          sdk[sl][c] = s; dk1[sl][c] = s; dk2[sl][c] = 3.0f * s; dk3[sl][c] = 3.0f * s;
+          accy[sl][c] = a[sl][c];
+        }
+      });
+
+      for (int jj = 3; jj >= 0; --jj) {
+        // stage input from the forward's checkpoint
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          if (p < M::PAIRS) {
+            const int r = p / TT, t = p - r * TT;
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+              lds[t * SR + M::Y_OFF + 3 * r + c] = A.ckpt[ckpt_index(tile, A.n_steps, step, jj, M::F, 3 * r + c, t)];
+          }
+        });
+        __syncthreads();
+        mlp_forward<M, W, SR>(A.pack, lds, c1, lane);
+
+        // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          dyf[sl][0] = dyf[sl][1] = 0.f;
+          if (p < M::PAIRS) {
+            const int r = p / TT, t = p - r * TT;
+            const bool valid = n0 + t < A.n_traj;
+            float* rec = lds + t * SR;
+            float Y[3], dres[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              Y[c] = rec[M::Y_OFF + 3 * r + c];
+              const float dk = jj == 3 ? sdk[sl][c] : jj == 2 ? dk3[sl][c] : jj == 1 ? dk2[sl][c] : dk1[sl][c];
+              dres[c] = (!valid || Y[c] > 2.f || Y[c] < -1.f) ? 0.f : dk;
+            }
+            if constexpr (M::HAS_A) {
+              constexpr int fo = M::act_off(1, M::nl(1) - 1);
+              constexpr int go = M::gbuf(1, M::nl(1) - 1);
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                const float fa = rec[fo + 3 * r + c];
+                float dfa = M::HAS_P ? A.fa_w * dres[c] : dres[c];
+                dfa = valid ? dfa + cn * fa : 0.f;
+                rec[go + 3 * r + c] = dfa;
+              }
+            }
+            if constexpr (M::HAS_P) {
+              constexpr int qo = M::act_off(0, M::nl(0) - 1);
+              constexpr int go = M::gbuf(0, M::nl(0) - 1);
+              const float q0 = rec[qo + 2 * r], q1 = rec[qo + 2 * r + 1];
+              const float b = fabsf(q0), gm = fabsf(q1);
+              const float dplus = dres[1] - dres[0];
+              const float dminus = dres[2] - dres[1];
+              const float dpi = dplus * Y[1];                 // d(beta*S)
+              float dbeta = dpi * Y[0];
+              const float dS = dpi * b;
+              const float dI = dplus * (b * Y[0]) + dminus * gm;
+              float dgam = dminus * Y[1];
+              if (valid) {
+                dbeta += ca[0] + cb[0] * (b - mu[0]);
+                dgam += ca[1] + cb[1] * (gm - mu[1]);
+              } else {
+                dbeta = 0.f; dgam = 0.f;
+              }
+              rec[go + 2 * r] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
+              rec[go + 2 * r + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
+              dyf[sl][0] = dS; dyf[sl][1] = dI;
+            }
+          }
+        });
+        // zero the padded rows of the final-layer gradient slots
+        if constexpr (M::HAS_P) {
+          constexpr int lo = 2 * M::R, hi = M::kout(0, M::nl(0) - 1);
+          for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
+            const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
+            lds[t * SR + M::gbuf(0, M::nl(0) - 1) + o] = 0.f;
+          }
+        }
+        if constexpr (M::HAS_A) {
+          constexpr int lo = 3 * M::R, hi = M::kout(1, M::nl(1) - 1);
+          for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
+            const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
+            lds[t * SR + M::gbuf(1, M::nl(1) - 1) + o] = 0.f;
+          }
+        }
+        __syncthreads();
+        mlp_backward<M, W, SR>(A.pack, lds, dw, gacc, g0t, lane);
+
+        // RK4 (3/8 rule) adjoint of the stage combination
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          if (p < M::PAIRS) {
+            const int r = p / TT, t = p - r * TT;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              float dY = lds[t * SR + M::GY_OFF + 3 * r + c];
+              if (c < 2) dY += dyf[sl][c];
+              accy[sl][c] += dY;
+              if (jj == 3) {
+                const float u = dt * dY;
+                dk1[sl][c] += u; dk2[sl][c] -= u; dk3[sl][c] += u;
+              } else if (jj == 2) {
+                const float u = dt * dY;
+                dk2[sl][c] += u; dk1[sl][c] -= u * (1.0f / 3.0f);
+              } else if (jj == 1) {
+                dk1[sl][c] += (dY * (1.0f / 3.0f)) * dt;
+              }
+            }
+          }
+        });
+      }
+#pragma unroll
+      for (int sl = 0; sl < SL; ++sl)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a[sl][c] = accy[sl][c] + pend[sl][c];
+    }
+
+    // ---- tile end: dy0 (dynamic), static-feature gradients, bias sums ----
+    sfor<SL>([&](auto ss) {
+      constexpr int sl = decltype(ss)::value;
+      const int p = tid + sl * NTHREADS;
+      if (p < M::PAIRS) {
+        const int r = p / TT, t = p - r * TT;
+        const int n = n0 + t;
+        if (n < A.n_traj) {
+          const size_t base = ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) A.dy0[base + c] = a[sl][c] + A.dlatent[base + c];
+        }
+      }
+    });
+    __syncthreads();
+    sfor<M::FT(0)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(0, k) == W) {
+        *reinterpret_cast<f4*>(lds + t16 * SR + M::G0_OFF + k * 16 + g * 4) = g0t[M::nz_before(W, k)];
+      }
+    });
+    load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    __syncthreads();
+    if constexpr (M::S > 0) {
+      // dW0[:, static] += sum_t G0[t][o] * x_static[t][s]   (read-modify-write of this WG's slab)
+      sfor<M::FT(0)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(0, k) == W) {
+          float ga[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + M::G0_OFF + k * 16 + t16];
+          for (int cs = 0; cs < M::NCS; ++cs) {
+            f4* dst = reinterpret_cast<f4*>(myslab + M::SLAB_STATIC + (k * M::NCS + cs) * 256) + lane;
+            f4 acc = *dst;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc = mfma4(ga[s], lds[(4 * g + s) * SR + M::XSB_OFF + cs * 16 + t16], acc);
+            *dst = acc;
+          }
+        }
+      });
+      // dy0[:, static] = W0[:, static]^T G0 + sum_j dlatent[j][:, static]
+      for (int rt = (tid >> 6); rt < M::NCS; rt += WAVES) {
+        f4 acc = gemm_tile<M::K0>(A.pack + M::WST_OFF + rt * (M::K0 / 16) * 256, lds + t16 * SR + M::G0_OFF, lane, f4zero());
+        const int n = n0 + t16;
+        if (n < A.n_traj) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int s = rt * 16 + g * 4 + e;
+            if (s < M::S) {
+              const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
+              const size_t base = ((size_t)n * M::R + r) * M::L + c;
+              float v = acc[e];
+              for (int jo = 0; jo <= A.n_out; ++jo) v += A.dlatent[(size_t)jo * NRL + base];
+              A.dy0[base] = v;
+            }
+          }
+        }
+      }
+    }
+    sfor<M::FT(0)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(0, k) == W) gacc[M::ng_before(W, 0, k)] += g0t[M::nz_before(W, k)];
+    });
+    __syncthreads();
+  }
+
+  // ---- kernel end: register tiles -> this workgroup's slab ----
+  sfor<M::D>([&](auto dd) {
+    constexpr int d = decltype(dd)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k);
+        sfor<M::rti(net, d)>([&](auto cc) {
+          constexpr int ct = decltype(cc)::value;
+          reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
+        });
+        f4 gv = gacc[M::ng_before(W, d, k)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = gv[e];
+          v += __shfl_xor(v, 1, 64); v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64); v += __shfl_xor(v, 8, 64);
+          gv[e] = v;
+        }
+        if (t16 == 0) *reinterpret_cast<f4*>(myslab + M::SLAB_DB + (M::FTbase(d) + k) * 16 + g * 4) = gv;
+      }
+    });
+  });
+}
+
+template <class M>
+__global__ __launch_bounds__(NTHREADS) void ude_bwd_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w == 0) bwd_body<M, 0>(a, lds);
+  else if (w == 1) bwd_body<M, 1>(a, lds);
+  else if (w == 2) bwd_body<M, 2>(a, lds);
+  else bwd_body<M, 3>(a, lds);
+}
+
+// ============================================================================
+// Weight packing (one launch, blockIdx.y = segment)
+// ============================================================================
+struct PackPtrs {
+  const float* W[2][5];
+  const float* b[2][5];
+};
+
+template <class M>
+__device__ __forceinline__ int in_col(int i, int f) {
+  // layer-0 dynamic feature f = 3r + c  ->  torch column r*L + c
+  return i == 0 ? (f / 3) * M::L + (f % 3) : f;
+}
+template <class M>
+__device__ __forceinline__ int static_col(int s) {
+  const int r = s / (M::L - 3);
+  return r * M::L + 3 + (s - r * (M::L - 3));
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __restrict__ pack) {
+  const int seg = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  sfor<2>([&](auto nn) {
+    constexpr int net = decltype(nn)::value;
+    sfor<5>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (M::has(net, i)) {
+        constexpr int base = (net * 5 + i) * 3;
+        constexpr int in = M::in_dim(net, i), out = M::out_dim(net, i);
+        constexpr int in_full = i == 0 ? M::R * M::L : in;
+        const float* Wp = P.W[net][i];
+        if (seg == base + 0 && idx < M::wf_size(net, i)) {
+          constexpr int KQ = M::kin(net, i) / 4, NQ = M::kin(net, i) / 16;
+          const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
+          const int o = rt * 16 + (ln & 15), f = (ln >> 4) * KQ + 4 * q + e;
+          pack[M::wf_off(net, i) + idx] = (o < out && f < in) ? Wp[(size_t)o * in_full + in_col<M>(i, f)] : 0.f;
+        } else if (seg == base + 1 && idx < M::wt_size(net, i)) {
+          constexpr int KQ = M::kout(net, i) / 4, NQ = M::kout(net, i) / 16;
+          const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
+          const int o = (ln >> 4) * KQ + 4 * q + e, f = rt * 16 + (ln & 15);
+          pack[M::wt_off(net, i) + idx] = (o < out && f < in) ? Wp[(size_t)o * in_full + in_col<M>(i, f)] : 0.f;
+        } else if (seg == base + 2 && idx < M::b_size(net, i)) {
+          pack[M::b_off(net, i) + idx] = idx < out ? P.b[net][i][idx] : 0.f;
+        }
+      }
+    });
+    if constexpr (M::S > 0 && M::has(net, 0)) {
+      if (seg == 30 + net && idx < M::wsf_size(net)) {
+        constexpr int KQ = M::S16 / 4, NQ = M::S16 / 16;
+        constexpr int out = M::out_dim(net, 0);
+        const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
+        const int o = rt * 16 + (ln & 15), s = (ln >> 4) * KQ + 4 * q + e;
+        pack[M::wsf_off(net) + idx] =
+            (o < out && s < M::S) ? P.W[net][0][(size_t)o * M::R * M::L + static_col<M>(s)] : 0.f;
+      }
+    }
+  });
+  if constexpr (M::S > 0) {
+    if (seg == 32 && idx < M::WST_SIZE) {
+      constexpr int KQ = M::K0 / 4, NQ = M::K0 / 16;
+      const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
+      int om = (ln >> 4) * KQ + 4 * q + e;
+      const int s = rt * 16 + (ln & 15);
+      int net = 0;
+      if (!M::HAS_P || om >= (M::HAS_P ? M::kout(0, 0) : 0)) {
+        net = 1;
+        om -= M::HAS_P ? M::kout(0, 0) : 0;
+      }
+      const int out = M::out_dim(net, 0);
+      float v = 0.f;
+      if (s < M::S && om < out && (net == 0 ? M::HAS_P : M::HAS_A))
+        v = P.W[net][0][(size_t)om * M::R * M::L + static_col<M>(s)];
+      pack[M::WST_OFF + idx] = v;
+    }
+  }
+}
+
+// ============================================================================
+// Deterministic reductions over the per-workgroup partials
+// ============================================================================
+template <class M>
+__global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __restrict__ slab, int ngrid,
+                                                                float* __restrict__ dparams) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= M::N_PARAMS) return;
+  int off = -1;
+  sfor<2>([&](auto nn) {
+    constexpr int net = decltype(nn)::value;
+    sfor<5>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (M::has(net, i)) {
+        constexpr int in_full = i == 0 ? M::R * M::L : M::in_dim(net, i);
+        constexpr int out = M::out_dim(net, i);
+        constexpr int w0 = M::param_w_off(net, i);
+        constexpr int b0 = w0 + out * in_full;
+        constexpr int kbase = net == 0 ? 0 : M::rto(0, i);
+        if (e >= w0 && e < b0) {
+          const int o = (e - w0) / in_full, col = (e - w0) - o * in_full;
+          const int k = kbase + o / 16, row = o % 16;
+          int f = col;
+          bool stat = false;
+          if (i == 0) {
+            const int r = col / M::L, c = col - r * M::L;
+            if (c < 3) f = 3 * r + c;
+            else { f = r * (M::L - 3) + (c - 3); stat = true; }
+          }
+          const int lane = (row >> 2) * 16 + (f & 15), reg = row & 3;
+          if (!stat) off = (M::dyn_tiles_before(i, k) + f / 16) * 256 + lane * 4 + reg;
+          else off = M::SLAB_STATIC + (k * M::NCS + f / 16) * 256 + lane * 4 + reg;
+        } else if (e >= b0 && e < b0 + out) {
+          const int o = e - b0;
+          off = M::SLAB_DB + (M::FTbase(i) + kbase + o / 16) * 16 + (o % 16);
+        }
+      }
+    });
+  });
+  float s = 0.f;
+  for (int gi = 0; gi < ngrid; ++gi) s += slab[(size_t)gi * M::SLAB_TOTAL + off];
+  dparams[e] = s;
+}
+
+template <int V_ = 0>
+__global__ void ude_stats_finalize_kernel(const double* __restrict__ slab, int ngrid, double n_eval,
+                                          float* __restrict__ out) {
+  __shared__ double tot[5];
+  const int c = threadIdx.x;
+  if (c < 5) {
+    double s = 0.0;
+    for (int gi = 0; gi < ngrid; ++gi) s += slab[(size_t)gi * 5 + c];
+    tot[c] = s;
+  }
+  __syncthreads();
+  if (c < 2) {
+    const double m = tot[c] / n_eval;
+    const double var = (tot[2 + c] - n_eval * m * m) / (n_eval - 1.0);
+    out[c] = (float)m;
+    out[2 + c] = (float)sqrt(var > 0.0 ? var : 0.0);
+  }
+  if (c == 4) out[4] = (float)sqrt(tot[4]);
+}
+
+}  // namespace ude

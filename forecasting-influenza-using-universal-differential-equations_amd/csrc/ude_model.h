@@ -1,0 +1,196 @@
+// Compile-time description of one UDE right-hand side (lib/models.py Fp / Fa / FaFp)
+// and every derived layout the gfx950 kernels use.  All of it is constexpr so
+// that per-wave register tiles (dW accumulators, static-hoist tiles) are
+// indexed with compile-time constants and never spill to scratch.
+//
+// Reference layer rule (lib/models.py:118-124, :208-223): for hidden sizes
+// [h1..hk] the Linears are in->h1, h1->h2, ..., hk->out with an ELU after
+// Linear i only for i < k-1 (the last hidden Linear and the output Linear
+// have no activation).  P-net ("net"/"Fp_net") outputs 2R rates, A-net
+// ("aug_net") outputs 3R augmentation fluxes.
+#pragma once
+
+namespace ude {
+
+constexpr int WAVES = 4;     // waves per workgroup (one per SIMD)
+constexpr int TT = 16;       // trajectories per tile = the N of v_mfma_f32_16x16x4_f32
+constexpr int NTHREADS = WAVES * 64;
+
+constexpr int pad16(int x) { return (x + 15) & ~15; }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+enum : int { KIND_FP = 1, KIND_FA = 2, KIND_FAFP = 3 };
+
+template <int R_, int L_, int KIND_, int NPH_, int P0_, int P1_, int P2_, int P3_,
+          int NAH_, int A0_, int A1_, int A2_, int A3_>
+struct Model {
+  static constexpr int R = R_, L = L_, KIND = KIND_;
+  static constexpr bool HAS_P = (KIND & 1) != 0;
+  static constexpr bool HAS_A = (KIND & 2) != 0;
+  static constexpr int NPH = NPH_, NAH = NAH_;
+  static constexpr int F = 3 * R;            // dynamic features: S, I, R of every region
+  static constexpr int S = R * (L - 3);      // static features: latent dims >= 3 (zero derivative)
+  static constexpr int F16 = pad16(F);
+  static constexpr int S16 = pad16(S);
+
+  static constexpr int nl(int net) { return net == 0 ? (HAS_P ? NPH + 1 : 0) : (HAS_A ? NAH + 1 : 0); }
+  static constexpr int D = cmax(nl(0), nl(1));
+  static constexpr int nh(int net) { return net == 0 ? NPH : NAH; }
+  static constexpr int hid(int net, int i) {
+    return net == 0 ? (i == 0 ? P0_ : i == 1 ? P1_ : i == 2 ? P2_ : P3_)
+                    : (i == 0 ? A0_ : i == 1 ? A1_ : i == 2 ? A2_ : A3_);
+  }
+  static constexpr bool has(int net, int i) { return i >= 0 && i < nl(net); }
+  static constexpr int in_dim(int net, int i) { return i == 0 ? F : hid(net, i - 1); }
+  static constexpr int out_dim(int net, int i) { return i < nh(net) ? hid(net, i) : (net == 0 ? 2 * R : 3 * R); }
+  static constexpr bool act(int net, int i) { return i < nh(net) - 1; }
+  static constexpr int kin(int net, int i) { return pad16(in_dim(net, i)); }
+  static constexpr int kout(int net, int i) { return pad16(out_dim(net, i)); }
+  static constexpr int rto(int net, int i) { return has(net, i) ? kout(net, i) / 16 : 0; }
+  static constexpr int rti(int net, int i) { return has(net, i) ? kin(net, i) / 16 : 0; }
+  static constexpr int K0 = (HAS_P ? kout(0, 0) : 0) + (HAS_A ? kout(1, 0) : 0);  // merged layer-0 rows
+
+  // ---- forward row tiles at depth d: P tiles first, then A tiles -------------
+  static constexpr int FT(int d) { return rto(0, d) + rto(1, d); }
+  static constexpr int FTbase(int d) { int s = 0; for (int e = 0; e < d; ++e) s += FT(e); return s; }
+  static constexpr int fnet(int d, int k) { return k < rto(0, d) ? 0 : 1; }
+  static constexpr int frt(int d, int k) { return k < rto(0, d) ? k : k - rto(0, d); }
+  static constexpr int fowner(int d, int k) { return (FTbase(d) + k) % WAVES; }
+
+  // ---- input-gradient (dX) row tiles at depth d --------------------------------
+  // d > 0: rows are the inputs of layer d of each net; d == 0: the dynamic features
+  // (both nets' layer-0 contributions summed in one accumulator).
+  static constexpr int XT(int d) { return d == 0 ? F16 / 16 : rti(0, d) + rti(1, d); }
+  static constexpr int xnet(int d, int m) { return m < rti(0, d) ? 0 : 1; }
+  static constexpr int xrt(int d, int m) { return m < rti(0, d) ? m : m - rti(0, d); }
+  static constexpr int xowner(int d, int m) {
+    // start where the forward tiles of this depth stopped: spreads dW + dX work
+    return (FTbase(d) + FT(d) + m) % WAVES;
+  }
+
+  // ---- LDS record: one row of SR floats per trajectory ([t][feature]) ---------
+  static constexpr int Y_OFF = 0;
+  static constexpr int act_off(int net, int i) {
+    int o = F16;
+    for (int n = 0; n < 2; ++n)
+      for (int j = 0; j < nl(n); ++j) {
+        if (n == net && j == i) return o;
+        o += kout(n, j);
+      }
+    return o;
+  }
+  static constexpr int ACT_END = act_off(2, 0);
+  // tile-level aliases over the activation region (only live outside the step loop)
+  static constexpr int G0_OFF = F16;                // backward: merged layer-0 gradient sums
+  static constexpr int XSB_OFF = F16 + K0;          // backward: static features
+  static constexpr int XSF_OFF = F16;               // forward: static features
+  static constexpr int ALIAS_END = cmax(ACT_END, F16 + K0 + S16);
+  static constexpr int gbs(int net) {
+    int m = 0;
+    for (int j = 0; j < nl(net); ++j) m = cmax(m, kout(net, j));
+    return m;
+  }
+  static constexpr int gb_off(int net, int parity) {
+    return ALIAS_END + (net == 0 ? 0 : 2 * gbs(0)) + parity * gbs(net);
+  }
+  static constexpr int gbuf(int net, int i) { return gb_off(net, i & 1); }
+  static constexpr int GY_OFF = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);
+  static constexpr int REC_F = cmax(ACT_END, F16 + S16);
+  static constexpr int REC_B = GY_OFF + F16;
+  // row stride == 4 (mod 64) floats: conflict-free b128 fragment reads, and rows
+  // t and t+4 land 16 banks apart for the dW b32 reads.
+  static constexpr int stride(int n) { return ((n + 59) / 64) * 64 + 4; }
+  static constexpr int SR_F = stride(REC_F);
+  static constexpr int SR_B = stride(REC_B);
+  static constexpr int LDS_F = TT * SR_F * 4;
+  static constexpr int LDS_B = TT * SR_B * 4;
+
+  // ---- packed weights (fragment order, 16-B per lane per MFMA quad) --------------
+  //  WF(net,i): [rto][kin/16][64 lanes][4]   A operand of the forward GEMM
+  //  WT(net,i): [rti][kout/16][64][4]        A operand of the input-gradient GEMM
+  //  B(net,i):  [kout]                       bias, zero padded
+  //  WSF(net):  [rto(net,0)][S16/16][64][4]  layer-0 static columns (per-tile hoist)
+  //  WST:       [S16/16][K0/16][64][4]       layer-0 static columns, transposed, merged nets
+  static constexpr int wf_size(int net, int i) { return has(net, i) ? rto(net, i) * (kin(net, i) / 16) * 256 : 0; }
+  static constexpr int wt_size(int net, int i) { return has(net, i) ? rti(net, i) * (kout(net, i) / 16) * 256 : 0; }
+  static constexpr int b_size(int net, int i) { return has(net, i) ? kout(net, i) : 0; }
+  static constexpr int layer_pack_size(int net, int i) { return wf_size(net, i) + wt_size(net, i) + b_size(net, i); }
+  static constexpr int layer_pack_off(int net, int i) {
+    int o = 0;
+    for (int n = 0; n < 2; ++n)
+      for (int j = 0; j < nl(n); ++j) {
+        if (n == net && j == i) return o;
+        o += layer_pack_size(n, j);
+      }
+    return o;
+  }
+  static constexpr int wf_off(int net, int i) { return layer_pack_off(net, i); }
+  static constexpr int wt_off(int net, int i) { return layer_pack_off(net, i) + wf_size(net, i); }
+  static constexpr int b_off(int net, int i) { return wt_off(net, i) + wt_size(net, i); }
+  static constexpr int LAYERS_END = layer_pack_off(2, 0);
+  static constexpr int wsf_size(int net) { return (S > 0 && has(net, 0)) ? rto(net, 0) * (S16 / 16) * 256 : 0; }
+  static constexpr int wsf_off(int net) { return LAYERS_END + (net == 0 ? 0 : wsf_size(0)); }
+  static constexpr int WST_OFF = LAYERS_END + wsf_size(0) + wsf_size(1);
+  static constexpr int WST_SIZE = S > 0 ? (S16 / 16) * (K0 / 16) * 256 : 0;
+  static constexpr int PACK_TOTAL = WST_OFF + WST_SIZE;
+
+  // ---- per-workgroup gradient slab -------------------------------------------------
+  static constexpr int dyn_tiles_before(int d, int k) {
+    int s = 0;
+    for (int e = 0; e < D; ++e)
+      for (int kk = 0; kk < FT(e); ++kk) {
+        if (e == d && kk == k) return s;
+        s += rti(fnet(e, kk), e);
+      }
+    return s;
+  }
+  static constexpr int N_DYN_TILES = dyn_tiles_before(D, 0);
+  static constexpr int NCS = S16 / 16;
+  static constexpr int SLAB_STATIC = N_DYN_TILES * 256;
+  static constexpr int SLAB_DB = SLAB_STATIC + FT(0) * NCS * 256;
+  static constexpr int SLAB_TOTAL = SLAB_DB + FTbase(D) * 16;
+
+  // ---- per-wave register tiles -----------------------------------------------------
+  static constexpr int ndw_before(int w, int d, int k) {
+    int s = 0;
+    for (int e = 0; e < D; ++e)
+      for (int kk = 0; kk < FT(e); ++kk) {
+        if (e == d && kk == k) return s;
+        if (fowner(e, kk) == w) s += rti(fnet(e, kk), e);
+      }
+    return s;
+  }
+  static constexpr int NDW(int w) { return ndw_before(w, D, 0); }
+  static constexpr int ng_before(int w, int d, int k) {
+    int s = 0;
+    for (int e = 0; e < D; ++e)
+      for (int kk = 0; kk < FT(e); ++kk) {
+        if (e == d && kk == k) return s;
+        if (fowner(e, kk) == w) s += 1;
+      }
+    return s;
+  }
+  static constexpr int NG(int w) { return ng_before(w, D, 0); }
+  static constexpr int nz_before(int w, int k) {
+    int s = 0;
+    for (int kk = 0; kk < k; ++kk) if (fowner(0, kk) == w) s += 1;
+    return s;
+  }
+  static constexpr int NZ(int w) { return nz_before(w, FT(0)); }
+
+  // ---- parameters in torch order (nn.Linear weight (out,in) then bias) ----------------
+  static constexpr int param_w_off(int net, int i) {
+    int o = 0;
+    for (int n = 0; n < 2; ++n)
+      for (int j = 0; j < nl(n); ++j) {
+        if (n == net && j == i) return o;
+        o += out_dim(n, j) * (j == 0 ? R * L : in_dim(n, j)) + out_dim(n, j);
+      }
+    return o;
+  }
+  static constexpr int N_PARAMS = param_w_off(2, 0);
+  static constexpr int PAIRS = R * TT;
+  static constexpr int SLOTS = (PAIRS + NTHREADS - 1) / NTHREADS;
+};
+
+}  // namespace ude

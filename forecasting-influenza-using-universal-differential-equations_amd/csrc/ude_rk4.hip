@@ -1,0 +1,66 @@
+// C-ABI entry points (include/ude_rk4.h) over the compiled model configurations.
+// The registry (ude_registry.inc, generated at build time) lists one
+// ude::Entry per configuration object linked into this library.
+#include <hip/hip_runtime.h>
+#include "ude_rk4.h"
+#include "ude_entry.h"
+
+// This translation unit is host code only (no kernels are instantiated here).
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include "ude_registry.inc"   // extern const ude::Entry ude_entry_N; + kEntries[] / kNumEntries
+
+using ude::Entry;
+
+namespace {
+const ude::Entry* find(const UdeModelDesc* m) {
+  if (!m) return nullptr;
+  for (int i = 0; i < ude::kNumEntries; ++i)
+    if (ude::kEntries[i]->match(m)) return ude::kEntries[i];
+  return nullptr;
+}
+}  // namespace
+
+extern "C" {
+
+int ude_supported(const UdeModelDesc* m) { return find(m) ? 1 : 0; }
+
+int ude_query(const UdeModelDesc* m, const UdeProblem* p, int device, UdeSizes* out) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || !out) return UDE_E_INVALID;
+  return e->query(p, device, out);
+}
+
+int ude_pack_weights(const UdeModelDesc* m, const float* const* W, const float* const* b, float* pack,
+                     ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!W || !b || !pack) return UDE_E_INVALID;
+  return e->pack(W, b, pack, (hipStream_t)stream);
+}
+
+int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                    const float* y0, float* latent, float* ckpt, double* stats_slab, float* stats_out,
+                    ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 0) return UDE_E_INVALID;
+  return e->forward(p, pack, sched, y0, latent, ckpt, stats_slab, stats_out, (hipStream_t)stream);
+}
+
+int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                     const float* y0, const float* ckpt, const float* dlatent, const float* stats_out,
+                     const float* dstats, float* dy0, float* grad_slab, float* dparams, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 0) return UDE_E_INVALID;
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, stats_out, dstats, dy0, grad_slab, dparams,
+                     (hipStream_t)stream);
+}
+
+const char* ude_build_info(void) {
+  return "ude_rk4 gfx950: v_mfma_f32_16x16x4_f32, TT=16, 4 waves/WG, registry=" UDE_REGISTRY_TAG;
+}
+
+}  // extern "C"
+#endif  // !__HIP_DEVICE_COMPILE__

@@ -1,0 +1,9 @@
+"""MI355X-native UDE influenza forecaster: the batched RK4 solve of the SIR-UDE
+right-hand side (forward + backward through the solver) as gfx950 kernels,
+behind the reference's own API (lib/models.py classes, torchdiffeq.odeint).
+"""
+from .rhs import Fp, Fa, FaFp, UDE_CLASSES
+from .solvers import odeint, fusable
+from . import _native, configs
+
+__all__ = ["Fp", "Fa", "FaFp", "odeint", "fusable", "UDE_CLASSES"]

@@ -1,0 +1,230 @@
+"""Loader and builder for the gfx950 C-ABI library (include/ude_rk4.h).
+
+The library is built in-tree with hipcc (``build_prebuilt``), one object per
+model configuration of ``configs.PREBUILT`` compiled in parallel and linked
+into ``_build/libude_rk4.so``.  A configuration that is not prebuilt is
+compiled on first use into ``_build/jit/libude_rk4_<key>.so`` (same C-ABI,
+one registry entry).  There is no fallback: if no library for a model can be
+loaded, the fused solver raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import shutil
+import subprocess
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence
+
+from . import configs as _cfgs
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+INCLUDE = os.path.join(REPO_DIR, "include")
+BUILD = os.path.join(PKG_DIR, "_build")
+PREBUILT_LIB = os.path.join(BUILD, "libude_rk4.so")
+JIT_DIR = os.path.join(BUILD, "jit")
+ARCH = os.environ.get("UDE_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+HIP_FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}"]
+
+UDE_OK, UDE_E_UNSUPPORTED, UDE_E_INVALID, UDE_E_HIP = 0, -1, -2, -3
+_ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "invalid argument",
+         UDE_E_HIP: "HIP runtime error"}
+
+EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_rk4_forward",
+                    "ude_rk4_backward", "ude_build_info")
+
+
+class UdeModelDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_regions", ctypes.c_int32), ("latent_dim", ctypes.c_int32),
+                ("n_p_hidden", ctypes.c_int32), ("p_hidden", ctypes.c_int32 * 4),
+                ("n_a_hidden", ctypes.c_int32), ("a_hidden", ctypes.c_int32 * 4)]
+
+
+class UdeProblem(ctypes.Structure):
+    _fields_ = [("n_traj", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("n_out", ctypes.c_int32),
+                ("fa_w", ctypes.c_float)]
+
+
+class UdeSizes(ctypes.Structure):
+    _fields_ = [("pack_bytes", ctypes.c_int64), ("sched_bytes", ctypes.c_int64), ("ckpt_bytes", ctypes.c_int64),
+                ("stats_slab_bytes", ctypes.c_int64), ("grad_slab_bytes", ctypes.c_int64),
+                ("n_params", ctypes.c_int64), ("grid_fwd", ctypes.c_int32), ("grid_bwd", ctypes.c_int32),
+                ("lds_fwd", ctypes.c_int32), ("lds_bwd", ctypes.c_int32)]
+
+
+def make_desc(cfg: _cfgs.Config) -> UdeModelDesc:
+    kind, R, L, net, aug = cfg
+    d = UdeModelDesc()
+    d.kind = _cfgs.KIND_CODE[kind]
+    d.n_regions = R
+    d.latent_dim = L
+    net = list(net or [])
+    aug = list(aug or [])
+    d.n_p_hidden = len(net)
+    d.n_a_hidden = len(aug)
+    for i, v in enumerate(net):
+        d.p_hidden[i] = v
+    for i, v in enumerate(aug):
+        d.a_hidden[i] = v
+    return d
+
+
+class UdeError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != UDE_OK:
+        raise UdeError(f"{what} failed: {_ERRS.get(rc, rc)} (code {rc})")
+
+
+class NativeLib:
+    """ctypes view of one libude_rk4*.so."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.lib = ctypes.CDLL(path)
+        L = self.lib
+        vp, i32 = ctypes.c_void_p, ctypes.c_int
+        pdesc, pprob = ctypes.POINTER(UdeModelDesc), ctypes.POINTER(UdeProblem)
+        L.ude_supported.argtypes = [pdesc]
+        L.ude_supported.restype = i32
+        L.ude_query.argtypes = [pdesc, pprob, i32, ctypes.POINTER(UdeSizes)]
+        L.ude_query.restype = i32
+        L.ude_pack_weights.argtypes = [pdesc, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
+        L.ude_pack_weights.restype = i32
+        L.ude_rk4_forward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_rk4_forward.restype = i32
+        L.ude_rk4_backward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_rk4_backward.restype = i32
+        L.ude_build_info.argtypes = []
+        L.ude_build_info.restype = ctypes.c_char_p
+
+    def supported(self, desc: UdeModelDesc) -> bool:
+        return bool(self.lib.ude_supported(ctypes.byref(desc)))
+
+    def query(self, desc, prob, device: int) -> UdeSizes:
+        out = UdeSizes()
+        check(self.lib.ude_query(ctypes.byref(desc), ctypes.byref(prob), int(device), ctypes.byref(out)), "ude_query")
+        return out
+
+    def pack(self, desc, w_ptrs: Sequence[int], b_ptrs: Sequence[int], pack_ptr: int, stream: int) -> None:
+        n = len(w_ptrs)
+        W = (ctypes.c_void_p * n)(*w_ptrs)
+        B = (ctypes.c_void_p * n)(*b_ptrs)
+        check(self.lib.ude_pack_weights(ctypes.byref(desc), W, B, pack_ptr, stream), "ude_pack_weights")
+
+    def forward(self, desc, prob, pack, sched, y0, latent, ckpt, stats_slab, stats_out, stream) -> None:
+        check(self.lib.ude_rk4_forward(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, latent, ckpt,
+                                       stats_slab, stats_out, stream), "ude_rk4_forward")
+
+    def backward(self, desc, prob, pack, sched, y0, ckpt, dlatent, stats_out, dstats, dy0, slab, dparams,
+                 stream) -> None:
+        check(self.lib.ude_rk4_backward(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
+                                        stats_out, dstats, dy0, slab, dparams, stream), "ude_rk4_backward")
+
+    def build_info(self) -> str:
+        return self.lib.ude_build_info().decode()
+
+
+# ---------------------------------------------------------------------------
+# building
+# ---------------------------------------------------------------------------
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise UdeError("build command failed:\n" + " ".join(cmd) + "\n" + r.stdout[-8000:])
+
+
+def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: Optional[int] = None) -> str:
+    """Compile one object per configuration + the C-ABI, link into out_path."""
+    if not os.path.exists(HIPCC):
+        raise UdeError(f"hipcc not found ({HIPCC}); cannot build the gfx950 library")
+    gen = os.path.join(BUILD, "gen_" + tag)
+    os.makedirs(gen, exist_ok=True)
+    reg = ["// generated by ude_amd/_native.py -- do not edit", "namespace ude {"]
+    reg += [f"extern const Entry ude_entry_{i};" for i in range(len(cfgs))]
+    reg.append("const Entry* const kEntries[] = {" + ", ".join(f"&ude_entry_{i}" for i in range(len(cfgs))) + "};")
+    reg.append(f"constexpr int kNumEntries = {len(cfgs)};")
+    reg.append("}  // namespace ude")
+    reg.append(f'#define UDE_REGISTRY_TAG "{tag}:{len(cfgs)}"')
+    with open(os.path.join(gen, "ude_registry.inc"), "w") as f:
+        f.write("\n".join(reg) + "\n")
+    inc = ["-I", INCLUDE, "-I", CSRC, "-I", gen]
+
+    def compile_cfg(i_cfg):
+        i, cfg = i_cfg
+        obj = os.path.join(gen, f"cfg_{i}.o")
+        _run([HIPCC, *HIP_FLAGS, *inc, "-c", os.path.join(CSRC, "ude_cfg.hip"), f"-DUDE_CFG_ID={i}",
+              f"-DUDE_ONE_CONFIG={_cfgs.template_args(cfg)}", "-o", obj])
+        return obj
+
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_cfg, list(enumerate(cfgs))))
+    capi = os.path.join(gen, "ude_rk4.o")
+    _run([HIPCC, *HIP_FLAGS, *inc, "-c", os.path.join(CSRC, "ude_rk4.hip"), "-o", capi])
+    tmp = out_path + ".tmp"
+    _run([HIPCC, *HIP_FLAGS, "-shared", *objs, capi, "-o", tmp])
+    os.replace(tmp, out_path)
+    return out_path
+
+
+def build_prebuilt(jobs: Optional[int] = None) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    return build_library(_cfgs.PREBUILT, PREBUILT_LIB, "prebuilt", jobs)
+
+
+# ---------------------------------------------------------------------------
+# loading
+# ---------------------------------------------------------------------------
+
+_lock = threading.Lock()
+_loaded: Dict[str, NativeLib] = {}
+
+
+def _load(path: str) -> NativeLib:
+    with _lock:
+        if path not in _loaded:
+            _loaded[path] = NativeLib(path)
+        return _loaded[path]
+
+
+def prebuilt() -> NativeLib:
+    if not os.path.exists(PREBUILT_LIB):
+        raise UdeError(f"{PREBUILT_LIB} is missing: run __graft_entry__.build() (hipcc, gfx950)")
+    return _load(PREBUILT_LIB)
+
+
+def jit_library(cfg: _cfgs.Config) -> NativeLib:
+    key = _cfgs.config_key(cfg)
+    h = hashlib.sha1(open(os.path.join(CSRC, "ude_kernels.h"), "rb").read()
+                     + open(os.path.join(CSRC, "ude_model.h"), "rb").read()).hexdigest()[:10]
+    path = os.path.join(JIT_DIR, f"libude_rk4_{key}_{h}.so")
+    if not os.path.exists(path):
+        os.makedirs(JIT_DIR, exist_ok=True)
+        build_library([cfg], path, f"jit_{key}_{h}", jobs=1)
+    return _load(path)
+
+
+def library_for(cfg: _cfgs.Config) -> NativeLib:
+    """The library that has a kernel for this configuration (JIT-compiling if needed)."""
+    desc = make_desc(cfg)
+    if os.path.exists(PREBUILT_LIB):
+        lib = prebuilt()
+        if lib.supported(desc):
+            return lib
+    lib = jit_library(cfg)
+    if not lib.supported(desc):
+        raise UdeError(f"no gfx950 kernel for {cfg}")
+    return lib
+
+
+def loaded_paths() -> List[str]:
+    return sorted(_loaded)

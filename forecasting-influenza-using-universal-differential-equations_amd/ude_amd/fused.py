@@ -1,0 +1,101 @@
+"""torch.autograd.Function over the C-ABI: one fused RK4 solve (+ its VJP).
+
+Forward : pack weights -> ude_rk4_forward (latent, stage checkpoints, side stats)
+Backward: ude_rk4_backward (dy0, every weight/bias gradient) -> split into the
+          parameters' shapes.
+PyTorch only provides device memory and the current HIP stream here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _native
+from .schedule import Schedule
+
+
+@dataclass
+class Plan:
+    lib: "_native.NativeLib"
+    desc: "_native.UdeModelDesc"
+    prob: "_native.UdeProblem"
+    sizes: "_native.UdeSizes"
+    sched_dev: torch.Tensor
+    n_times: int
+    n_eval: int
+    param_shapes: List[torch.Size]
+
+
+def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.device,
+              param_shapes: List[torch.Size]) -> Plan:
+    lib = _native.library_for(cfg)
+    desc = _native.make_desc(cfg)
+    prob = _native.UdeProblem()
+    prob.n_traj = int(n_traj)
+    prob.n_steps = schedule.n_steps
+    prob.n_out = schedule.n_out
+    prob.fa_w = float(fa_w)
+    dev_index = device.index if device.index is not None else torch.cuda.current_device()
+    sizes = lib.query(desc, prob, dev_index)
+    sched = torch.from_numpy(schedule.to_bytes()).to(device, non_blocking=False)
+    n_eval = 4 * schedule.n_steps * n_traj * cfg[1]
+    return Plan(lib, desc, prob, sizes, sched, schedule.n_times, n_eval, param_shapes)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class FusedRK4(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, plan: Plan, y0: torch.Tensor, *params: torch.Tensor):
+        dev = y0.device
+        stream = _stream(dev)
+        sz = plan.sizes
+        ws = [p.contiguous() for p in params[0::2]]
+        bs = [p.contiguous() for p in params[1::2]]
+        pack = torch.empty(sz.pack_bytes // 4, dtype=torch.float32, device=dev)
+        plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
+        latent = torch.empty((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
+        need_grad = any(ctx.needs_input_grad[1:])
+        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) if need_grad else None
+        stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
+        stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        plan.lib.forward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                         latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), stats.data_ptr(), stream)
+        ctx.plan = plan
+        if need_grad:
+            ctx.save_for_backward(y0, pack, ckpt, stats)
+        return latent, stats
+
+    @staticmethod
+    def backward(ctx, dlatent, dstats):
+        plan: Plan = ctx.plan
+        y0, pack, ckpt, stats = ctx.saved_tensors
+        dev = y0.device
+        stream = _stream(dev)
+        if dlatent is None:
+            dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
+        dlatent = dlatent.contiguous().to(torch.float32)
+        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+        dy0 = torch.empty_like(y0)
+        slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
+        plan.lib.backward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                          ckpt.data_ptr(), dlatent.data_ptr(), stats.data_ptr(), dstats.data_ptr(),
+                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        grads = []
+        off = 0
+        for shp in plan.param_shapes:
+            n = 1
+            for s in shp:
+                n *= s
+            grads.append(dparams[off:off + n].view(shp))
+            off += n
+        return (None, dy0) + tuple(grads)

@@ -1,0 +1,204 @@
+"""UDE right-hand sides with the reference's module interface.
+
+Same class names, constructor signatures, attributes and ``state_dict`` keys as
+``lib/models.py``: ``Fp`` (:109-156, keys ``Fp_net.{1,3,..}``), ``Fa``
+(:158-197, ``aug_net.{0,2,..}``), ``FaFp`` (:199-265, ``net.*`` /
+``aug_net.*``), so reference checkpoints load unchanged and, under the same
+torch seed, the default initialisation draws the same weights.
+
+``forward(t, x)`` is one eager evaluation with the reference semantics (used
+when the module is called directly or by a non-fused solver).  Inside
+``odeint(..., method='rk4')`` on a HIP device the whole solve runs in the
+fused gfx950 kernel instead; the kernel then returns the side statistics the
+loss reads (rate mean / std for ``posterior()``, the Fa norm for ``tracker``)
+rather than per-eval tensors, see ``_record_fused``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+from torch import nn
+from torch.distributions import Normal
+
+
+def _linear_stack(n_in: int, sizes: Sequence[int], n_out: int, lead_flatten: bool) -> nn.ModuleList:
+    """[Flatten?] Lin(n_in->s0) (ELU Lin(s_{i-1}->s_i))* Lin(s_last->n_out).
+
+    Module indices (and so state_dict keys) follow lib/models.py:118-124: the
+    ELU sits between consecutive hidden Linears only, so the last hidden Linear
+    feeds the output Linear without an activation.
+    """
+    mods: List[nn.Module] = [nn.Flatten()] if lead_flatten else []
+    widths = [n_in] + list(sizes)
+    mods.append(nn.Linear(widths[0], widths[1]))
+    for a, b in zip(widths[1:-1], widths[2:]):
+        mods.extend([nn.ELU(inplace=True), nn.Linear(a, b)])
+    mods.append(nn.Linear(widths[-1], n_out))
+    return nn.ModuleList(mods)
+
+
+def _run_stack(stack, h: torch.Tensor) -> torch.Tensor:
+    for m in stack:
+        h = m(h)
+    return h
+
+
+def _sir_flux(rates: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """[-b S I, b S I - g I, g I] with rates (N,R,2) = [b, g] (lib/models.py:139-142)."""
+    infect = rates[..., 0] * x[..., 0] * x[..., 1]
+    recover = rates[..., 1] * x[..., 1]
+    return torch.stack([-infect, infect - recover, recover], dim=-1)
+
+
+def _finish(flux3: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """Append zero derivatives for dims >= 3 and zero entries outside [-1, 2]."""
+    res = torch.cat([flux3, torch.zeros_like(x[..., 3:])], -1)
+    res[(x > 2) | (x < -1)] = 0.0
+    return res
+
+
+class _UDEModule(nn.Module):
+    """Shared tracking / posterior logic of the three RHS classes."""
+
+    ode_type = "FaFp"
+    uncertainty = "none"
+
+    def _init_tracking(self):
+        self.params = []
+        self.tracker = []
+        self._fused_rates: List[Tuple[float, torch.Tensor, torch.Tensor]] = []
+
+    def clear_tracking(self):
+        """Resets the trackers (lib/models.py:148-150)."""
+        self.params = []
+        self.tracker = []
+        self._fused_rates = []
+
+    # -- fused-solver side statistics ------------------------------------------
+    def _record_fused(self, stats: torch.Tensor, n_eval: int) -> None:
+        """stats = [mean_b, mean_g, std_b, std_g, |Fa|] from one fused solve."""
+        if self.ode_type in ("Fp", "FaFp"):
+            self._fused_rates.append((float(n_eval), stats[0:2], stats[2:4]))
+        if self.ode_type in ("Fa", "FaFp"):
+            # torch.norm(torch.stack(tracker)) over this entry == |Fa| of the solve,
+            # and over several entries == the norm of all of them together.
+            self.tracker.append(stats[4:5])
+
+    def posterior(self) -> Normal:
+        """Normal(mean, unbiased std) of every recorded rate; clears them (:152-156)."""
+        groups = []
+        if self.params:
+            p = torch.stack(self.params).reshape(-1, 2)
+            groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
+        groups.extend(self._fused_rates)
+        self.params = []
+        self._fused_rates = []
+        if not groups:
+            torch.stack([])  # same error as the reference on an empty tracker
+        if len(groups) == 1:
+            _, m, s = groups[0]
+            return Normal(m, s)
+        n_tot = sum(g[0] for g in groups)
+        mean = sum(g[0] * g[1] for g in groups) / n_tot
+        ss = sum((g[0] - 1.0) * g[2] ** 2 + g[0] * (g[1] - mean) ** 2 for g in groups)
+        return Normal(mean, torch.sqrt(ss / (n_tot - 1.0)))
+
+    # -- description consumed by the fused solver -----------------------------
+    def ude_config(self):
+        net = tuple(self._p_sizes) if self.ode_type in ("Fp", "FaFp") else None
+        aug = tuple(self._a_sizes) if self.ode_type in ("Fa", "FaFp") else None
+        return (self.ode_type, self.n_regions, self.latent_dim, net, aug)
+
+    def ude_linears(self) -> List[nn.Linear]:
+        """Linears in C-ABI order: rate net layers, then augmentation net layers."""
+        out: List[nn.Linear] = []
+        if self.ode_type in ("Fp", "FaFp"):
+            out += [m for m in self._p_stack() if isinstance(m, nn.Linear)]
+        if self.ode_type in ("Fa", "FaFp"):
+            out += [m for m in self._a_stack() if isinstance(m, nn.Linear)]
+        return out
+
+    def fa_weight(self) -> float:
+        return float(getattr(self, "Fa_w", 1.0))
+
+
+class Fp(_UDEModule):
+    """Physics RHS with MLP-learned SIR rates ("CONN"), lib/models.py:109-156."""
+
+    def __init__(self, n_regions=1, latent_dim=8, net_sizes=[20, 20], **kwargs):
+        super().__init__()
+        self.n_regions = n_regions
+        self.latent_dim = latent_dim
+        self.ode_type = "Fp"
+        self.uncertainty = "none"
+        self._p_sizes = list(net_sizes)
+        self.Fp_net = _linear_stack(n_regions * latent_dim, net_sizes, 2 * n_regions, lead_flatten=True)
+        self._init_tracking()
+
+    def _p_stack(self):
+        return self.Fp_net
+
+    def forward(self, t, x):
+        rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
+        self.params.append(rates)
+        return _finish(_sir_flux(rates, x), x)
+
+
+class Fa(_UDEModule):
+    """Pure MLP RHS ("SONN"), lib/models.py:158-197."""
+
+    def __init__(self, n_regions=1, latent_dim=8, net_sizes=[32, 32], aug_net_sizes=[32, 32], nhidden_fa=32,
+                 **kwargs):
+        super().__init__()
+        self.ode_type = "Fa"
+        self.uncertainty = "none"
+        self.n_regions = n_regions
+        self.latent_dim = latent_dim
+        self.flatten = nn.Flatten()
+        self._a_sizes = list(aug_net_sizes)
+        self.aug_net = _linear_stack(n_regions * latent_dim, aug_net_sizes, 3 * n_regions, lead_flatten=False)
+        self._init_tracking()
+
+    def _a_stack(self):
+        return self.aug_net
+
+    def forward(self, t, x):
+        fa = _run_stack(self.aug_net, self.flatten(x)).reshape(-1, self.n_regions, 3)
+        res = _finish(fa, x)
+        self.tracker.append(fa)
+        return res
+
+
+class FaFp(_UDEModule):
+    """Physics + MLP augmentation RHS ("UONN"), lib/models.py:199-265."""
+
+    def __init__(self, n_regions=1, latent_dim=8, net_sizes=[20, 20], aug_net_sizes=[32, 32], **kwargs):
+        super().__init__()
+        self.n_regions = n_regions
+        self.latent_dim = latent_dim
+        self.ode_type = "FaFp"
+        self.uncertainty = "none"
+        self._p_sizes = list(net_sizes)
+        self._a_sizes = list(aug_net_sizes)
+        self.net = _linear_stack(n_regions * latent_dim, net_sizes, 2 * n_regions, lead_flatten=True)
+        self.aug_net = _linear_stack(n_regions * latent_dim, aug_net_sizes, 3 * n_regions, lead_flatten=True)
+        self.Fa_w = 1.0
+        self._init_tracking()
+
+    def _p_stack(self):
+        return self.net
+
+    def _a_stack(self):
+        return self.aug_net
+
+    def forward(self, t, x):
+        rates = torch.abs(_run_stack(self.net, x)).reshape(-1, self.n_regions, 2)
+        self.params.append(rates)
+        fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
+        res = _finish(_sir_flux(rates, x) + self.Fa_w * fa, x)
+        self.tracker.append(fa)
+        return res
+
+
+UDE_CLASSES = (Fp, Fa, FaFp)

@@ -1,0 +1,127 @@
+"""``odeint`` with torchdiffeq's signature (the reference's solver API).
+
+``odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None,
+event_fn=None)`` as imported by lib/VAE.py:5 and run_ode.py:24 and called as
+``odeint(ode, z, t, method='rk4', options=dict(step_size=h))``
+(lib/VAE.py:137, tuning/tune_encoders.py:221, tuning/tune_node.py:204).
+
+Dispatch:
+* ``method='rk4'`` + an RHS of this package (Fp / Fa / FaFp) + fp32 state on a
+  HIP device  ->  the fused gfx950 kernel (forward + VJP), no fallback: a
+  missing or unloadable library raises;
+* anything else (other callables, CPU tensors, fixed-grid 'euler' /
+  'midpoint' / 'rk4')  ->  the generic step-by-step solver below, which calls
+  ``func`` once per stage exactly as torchdiffeq does.  Setting
+  ``UDE_STRICT=1`` makes a UDE module that would take this path raise instead.
+Adaptive methods (dopri5, ...) are recognised but not implemented yet.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from .rhs import _UDEModule
+from .schedule import build_schedule, fixed_grid
+from . import fused as _fused
+
+FIXED_METHODS = ("rk4", "euler", "midpoint")
+ADAPTIVE_METHODS = ("dopri8", "dopri5", "bosh3", "fehlberg2", "adaptive_heun", "explicit_adams",
+                    "implicit_adams", "fixed_adams", "scipy_solver")
+ONE_THIRD = 1.0 / 3.0
+TWO_THIRDS = 2.0 / 3.0
+
+
+def _check_t(t: torch.Tensor) -> None:
+    if not torch.is_tensor(t):
+        raise TypeError("t must be a torch.Tensor")
+    if t.dim() != 1:
+        raise AssertionError("t must be one dimensional")
+    if not torch.is_floating_point(t):
+        raise TypeError("t must be a floating point Tensor")
+    if len(t) > 1 and not bool((t[1:] > t[:-1]).all()):
+        raise AssertionError("t must be strictly increasing")
+
+
+def fusable(func, y0: torch.Tensor) -> bool:
+    return (isinstance(func, _UDEModule) and func.uncertainty == "none" and y0.is_cuda
+            and y0.dtype == torch.float32 and y0.dim() == 3
+            and y0.shape[1] == func.n_regions and y0.shape[2] == func.latent_dim
+            and all(p.is_cuda and p.dtype == torch.float32 for p in func.parameters()))
+
+
+def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=None) -> torch.Tensor:
+    sched = build_schedule(t, step_size)
+    lins = func.ude_linears()
+    params = []
+    for lin in lins:
+        params += [lin.weight, lin.bias]
+    plan = _fused.make_plan(func.ude_config(), sched, y0.shape[0], func.fa_weight(), y0.device,
+                            [p.shape for p in params])
+    latent, stats = _fused.FusedRK4.apply(plan, y0.contiguous(), *params)
+    func._record_fused(stats, plan.n_eval)
+    return latent
+
+
+def _step_rk4(func, t0, dt, t1, y):
+    k1 = func(t0, y)
+    k2 = func(t0 + dt * ONE_THIRD, y + dt * k1 * ONE_THIRD)
+    k3 = func(t0 + dt * TWO_THIRDS, y + dt * (k2 - k1 * ONE_THIRD))
+    k4 = func(t1, y + dt * (k1 - k2 + k3))
+    return (k1 + 3 * (k2 + k3) + k4) * dt * 0.125
+
+
+def _step_euler(func, t0, dt, t1, y):
+    return dt * func(t0, y)
+
+
+def _step_midpoint(func, t0, dt, t1, y):
+    half = 0.5 * dt
+    return dt * func(t0 + half, y + func(t0, y) * half)
+
+
+_STEPS = {"rk4": _step_rk4, "euler": _step_euler, "midpoint": _step_midpoint}
+
+
+def eager_fixed_grid(func, y0, t, method="rk4", step_size=None):
+    step = _STEPS[method]
+    grid = fixed_grid(t, step_size).to(y0.device)
+    tt = t.to(y0.device)
+    out = [y0]
+    j = 1
+    y = y0
+    for n in range(len(grid) - 1):
+        t0, t1 = grid[n], grid[n + 1]
+        dt = t1 - t0
+        y1 = y + step(func, t0, dt, t1, y)
+        while j < len(tt) and t1 >= tt[j]:
+            if tt[j] == t0:
+                out.append(y)
+            elif tt[j] == t1:
+                out.append(y1)
+            else:
+                out.append(y + (tt[j] - t0) / (t1 - t0) * (y1 - y))
+            j += 1
+        y = y1
+    return torch.stack(out, 0)
+
+
+def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None):
+    if event_fn is not None:
+        raise NotImplementedError("event handling is not supported")
+    method = "dopri5" if method is None else method
+    if method not in FIXED_METHODS + ADAPTIVE_METHODS:
+        raise ValueError('Invalid method "{}". Must be one of {}'.format(
+            method, '{"' + '", "'.join(FIXED_METHODS + ADAPTIVE_METHODS) + '"}.'))
+    _check_t(t)
+    options = dict(options or {})
+    step_size = options.pop("step_size", None)
+    if method in ADAPTIVE_METHODS:
+        raise NotImplementedError(f"method '{method}' is not implemented yet (fixed-grid rk4/euler/midpoint are)")
+    if method == "rk4" and fusable(func, y0):
+        return fused_odeint(func, y0, t, step_size)
+    if isinstance(func, _UDEModule) and os.environ.get("UDE_STRICT", "0") == "1":
+        raise RuntimeError("UDE_STRICT=1: this solve would not run on the fused gfx950 kernel "
+                           f"(method={method}, device={y0.device}, dtype={y0.dtype})")
+    return eager_fixed_grid(func, y0, t, method, step_size)

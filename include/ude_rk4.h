@@ -1,0 +1,122 @@
+/*
+ * ude_rk4.h -- C-ABI of the MI355X (gfx950) UDE RK4 solver library.
+ *
+ * Drop-in boundary for the reference's hot path:
+ *   torchdiffeq.odeint(ode, z, t, method='rk4', options=dict(step_size=h))
+ *   called at lib/VAE.py:137 (and tuning/tune_encoders.py:221,
+ *   tuning/tune_node.py:204, tuning/tune_Fp.py:93), with `ode` one of the
+ *   right-hand sides Fp / Fa / FaFp of lib/models.py:109-265, plus the
+ *   autograd backward through that solve that lib/VAE.py:203
+ *   (`loss.backward()`) triggers, and the side statistics the loss reads:
+ *   ode.posterior() (lib/models.py:152-156, lib/VAE.py:173) and
+ *   torch.norm(torch.stack(ode.tracker)) (lib/VAE.py:180).
+ *
+ * Conventions
+ *   - every pointer is a device pointer (HBM) unless stated; the caller owns
+ *     every buffer, sized by ude_query(); the library never allocates and
+ *     keeps no state between calls (re-entrant, stream ordered);
+ *   - y0 / latent / dlatent / dy0 are row-major (..., N, R, L) fp32 exactly as
+ *     a contiguous torch tensor; weights are nn.Linear layout (out, in);
+ *   - return value 0 = ok, < 0 = error (UDE_E_*); the Python layer raises.
+ */
+#ifndef UDE_RK4_H
+#define UDE_RK4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* ude_stream_t; /* == hipStream_t */
+
+enum {
+  UDE_OK = 0,
+  UDE_E_UNSUPPORTED = -1, /* no compiled kernel for this model description */
+  UDE_E_INVALID = -2,     /* bad argument (sizes, null pointers)            */
+  UDE_E_HIP = -3          /* a HIP runtime call failed                      */
+};
+
+enum { UDE_KIND_FP = 1, UDE_KIND_FA = 2, UDE_KIND_FAFP = 3 };
+
+/* The RHS module: lib/models.py FaFp(n_regions, latent_dim, net_sizes,
+ * aug_net_sizes) etc.  Hidden-size lists of up to 4 entries. */
+typedef struct UdeModelDesc {
+  int32_t kind;          /* UDE_KIND_*                                   */
+  int32_t n_regions;     /* R                                            */
+  int32_t latent_dim;    /* L (>= 3)                                     */
+  int32_t n_p_hidden;    /* len(net_sizes), 0 if no P-net                */
+  int32_t p_hidden[4];
+  int32_t n_a_hidden;    /* len(aug_net_sizes), 0 if no A-net            */
+  int32_t a_hidden[4];
+} UdeModelDesc;
+
+/* One solve: N trajectories, `n_steps` RK4 grid steps, `n_out` output times. */
+typedef struct UdeProblem {
+  int32_t n_traj;
+  int32_t n_steps;
+  int32_t n_out;
+  float fa_w;            /* FaFp.Fa_w (lib/models.py:225)                */
+} UdeProblem;
+
+/* Buffer sizes in bytes for one (model, problem). */
+typedef struct UdeSizes {
+  int64_t pack_bytes;       /* packed weights                                  */
+  int64_t sched_bytes;      /* step/output schedule (layout below)              */
+  int64_t ckpt_bytes;       /* stage states saved by a training forward          */
+  int64_t stats_slab_bytes; /* per-workgroup fp64 partial sums                   */
+  int64_t grad_slab_bytes;  /* per-workgroup gradient partials                   */
+  int64_t n_params;         /* floats in the flat parameter-gradient output      */
+  int32_t grid_fwd;         /* workgroups launched by the forward                */
+  int32_t grid_bwd;         /* workgroups launched by the backward               */
+  int32_t lds_fwd;          /* bytes of LDS per workgroup                        */
+  int32_t lds_bwd;
+} UdeSizes;
+
+/*
+ * Schedule buffer (host-built, copied to the device), little-endian, packed:
+ *   float   dt[n_steps]            grid[n+1]-grid[n] in fp32 (torchdiffeq)
+ *   int32   out_start[n_steps+1]   CSR: outputs written after step n
+ *   int32   out_j[n_out]           output index (1..T-1; output 0 is y0)
+ *   int32   out_mode[n_out]        0: y(t0)  1: y(t1)  2: linear interpolation
+ *   float   out_slope[n_out]       (t_j - t0)/(t1 - t0) in fp32
+ * n_out here counts outputs 1..T-1 (T-1 entries).
+ */
+
+/* 1 if a kernel for this model is compiled into this library. */
+int ude_supported(const UdeModelDesc* m);
+
+/* Fill *out.  `device` is the HIP device ordinal used to size the grid. */
+int ude_query(const UdeModelDesc* m, const UdeProblem* p, int device, UdeSizes* out);
+
+/* Pack nn.Linear weights into the fragment layouts the kernels read.
+ * W[i] / b[i]: P-net layers first (i = 0..n_p_hidden), then A-net layers. */
+int ude_pack_weights(const UdeModelDesc* m, const float* const* W, const float* const* b,
+                     float* pack, ude_stream_t stream);
+
+/* Forward solve.  latent: (T, N, R, L) with T = n_out + 1.  If ckpt != NULL
+ * the stage states are saved for ude_rk4_backward.  stats_out (device, 5
+ * floats) receives {mean_beta, mean_gamma, std_beta, std_gamma, |Fa|}
+ * (entries of an absent net are 0). */
+int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
+                    const void* sched, const float* y0, float* latent, float* ckpt,
+                    double* stats_slab, float* stats_out, ude_stream_t stream);
+
+/* Backward (VJP) through the same solve.
+ *   dlatent: (T, N, R, L) cotangent of latent
+ *   dstats (device, 5 floats): d/dmean[2], d/dstd[2], d/d|Fa|
+ *   dy0: (N, R, L) written;  dparams: n_params floats, torch parameter order
+ *   (for each net: weight (out,in) then bias, layer by layer; P-net first). */
+int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
+                     const void* sched, const float* y0, const float* ckpt,
+                     const float* dlatent, const float* stats_out, const float* dstats,
+                     float* dy0, float* grad_slab, float* dparams, ude_stream_t stream);
+
+/* Library build tag (for logs / tests). */
+const char* ude_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UDE_RK4_H */

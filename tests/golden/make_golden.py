@@ -1,0 +1,180 @@
+"""Generate the golden fixtures under tests/golden/ (run in the build container).
+
+This is the ONLY place reference code runs.  It imports the reference's own RHS
+classes (``lib/models.py`` Fp / Fa / FaFp under /root/reference) and integrates
+them with the oracle's restatement of torchdiffeq's fixed-grid RK4 (torchdiffeq
+itself is absent from the reference and the image; see oracle/ude_oracle.py).
+The loss side-statistics are taken exactly as ``lib/VAE.py`` takes them:
+``ode.posterior()`` (:173) and ``torch.norm(torch.stack(ode.tracker))`` (:180).
+
+Outputs (npz, no pickles): inputs, reference-RHS outputs in fp32 and fp64, the
+VJP of a fixed linear functional in fp64, and the fp32-vs-fp64 distances the
+reference itself shows on each case (used to set the parity tolerance).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, "/root/reference")
+sys.dont_write_bytecode = True
+
+import lib.models as ref_models  # noqa: E402  (reference, read-only)
+from oracle.ude_oracle import odeint_rk4, normwise_rel  # noqa: E402
+
+CASES = [
+    # name, kind, R, L, net_sizes, aug_net_sizes, N, t-spec, step, fa_w, masked
+    ("fafp_r1_weekly", "FaFp", 1, 8, [64, 64, 32], [64, 64], 48, ("arange", 9, 1.0), "t1-t0", 1.0, False),
+    ("fp_r1_daily", "Fp", 1, 8, [32, 32], None, 40, ("arange", 29, 7.0), "t1-t0", 1.0, False),
+    ("fa_r1_weekly", "Fa", 1, 8, None, [64, 64], 24, ("arange", 6, 1.0), "t1-t0", 1.0, False),
+    ("fafp_r10_weekly", "FaFp", 10, 8, [64, 64, 32], [64, 64], 20, ("arange", 5, 1.0), "t1-t0", 1.0, False),
+    ("fafp_r49_weekly", "FaFp", 49, 8, [64, 64, 32], [64, 64], 8, ("arange", 3, 1.0), "t1-t0", 1.0, False),
+    ("fafp_r1_interp", "FaFp", 1, 8, [64, 64, 32], [64, 64], 24, ("linspace", 20, 7.0), 1.0, 0.05, False),
+    ("fafp_r1_masked", "FaFp", 1, 8, [64, 64, 32], [64, 64], 32, ("arange", 9, 1.0), "t1-t0", 1.0, True),
+    ("fafp_r1_defaults", "FaFp", 1, 8, [20, 20], [32, 32], 24, ("arange", 8, 7.0), "t1-t0", 1.0, False),
+    ("fp_r1_onehidden", "Fp", 1, 6, [24], None, 24, ("arange", 6, 1.0), "t1-t0", 1.0, False),
+    ("fafp_r3_l5_ragged", "FaFp", 3, 5, [40, 24], [36], 37, ("arange", 7, 3.0), "t1-t0", 0.5, False),
+]
+
+
+def make_t(spec):
+    kind, n, div = spec
+    if kind == "arange":
+        return torch.arange(n, dtype=torch.float32) / div
+    return torch.linspace(1, n, n) / div
+
+
+def make_y0(gen, N, R, L, masked):
+    S = torch.rand(N, R, generator=gen) * 0.4 + 0.5
+    I = torch.rand(N, R, generator=gen) * 0.05
+    Rr = 1 - S - I
+    rest = torch.randn(N, R, L - 3, generator=gen)
+    y0 = torch.cat([S[..., None], I[..., None], Rr[..., None], rest], -1) + 1e-5
+    if masked:
+        # push some compartments outside [-1, 2] (the strict mask of lib/models.py:130)
+        y0[0::4, :, 0] = 2.5
+        y0[1::4, :, 1] = -1.5
+        y0[2::4, :, 2] = 2.0      # exactly 2.0 is NOT masked
+    return y0.float()
+
+
+def build_module(kind, R, L, net, aug):
+    if kind == "FaFp":
+        return ref_models.FaFp(R, latent_dim=L, net_sizes=net, aug_net_sizes=aug)
+    if kind == "Fp":
+        return ref_models.Fp(R, latent_dim=L, net_sizes=net)
+    return ref_models.Fa(R, latent_dim=L, aug_net_sizes=aug)
+
+
+def run(mod, y0, t, step, dlatent, dmean, dstd, dnorm, dtype):
+    mod = mod.to(dtype)
+    y0 = y0.to(dtype).clone().requires_grad_(True)
+    if step == "t1-t0":
+        h = t[1] - t[0]
+    else:
+        h = step
+    mod.clear_tracking()
+    latent = odeint_rk4(mod, y0, t, h)
+    loss = (latent * dlatent.to(dtype)).sum()
+    out = {"latent": latent.detach()}
+    if mod.ode_type in ("Fa", "FaFp"):
+        norm = torch.norm(torch.stack(mod.tracker))          # lib/VAE.py:180
+        loss = loss + dnorm * norm
+        out["fa_norm"] = norm.detach().reshape(1)
+    if mod.ode_type in ("Fp", "FaFp"):
+        post = mod.posterior()                                # lib/VAE.py:173
+        loss = loss + (post.loc * dmean.to(dtype)).sum() + (post.scale * dstd.to(dtype)).sum()
+        out["mean"] = post.loc.detach()
+        out["std"] = post.scale.detach()
+    params = [p for _, p in mod.named_parameters()]
+    grads = torch.autograd.grad(loss, [y0] + params)
+    out["d_y0"] = grads[0]
+    for (name, _), g in zip(mod.named_parameters(), grads[1:]):
+        out["d_" + name] = g
+    mod.clear_tracking()
+    return out
+
+
+def main():
+    torch.set_num_threads(1)
+    for ci, (name, kind, R, L, net, aug, N, tspec, step, fa_w, masked) in enumerate(CASES):
+        torch.manual_seed(1000 + ci)
+        gen = torch.Generator().manual_seed(2000 + ci)
+        mod = build_module(kind, R, L, net, aug)
+        if kind == "FaFp":
+            mod.Fa_w = fa_w
+        t = make_t(tspec)
+        y0 = make_y0(gen, N, R, L, masked)
+        dlatent = torch.randn(len(t), N, R, L, generator=gen, dtype=torch.float64)
+        dmean = torch.tensor([0.3, -0.2], dtype=torch.float64)
+        dstd = torch.tensor([0.5, 0.1], dtype=torch.float64)
+        dnorm = 0.1
+        sd32 = {k: v.detach().clone() for k, v in mod.state_dict().items()}
+        import copy
+        o32 = run(copy.deepcopy(mod), y0, t, step, dlatent, dmean, dstd, dnorm, torch.float32)
+        o64 = run(copy.deepcopy(mod), y0, t, step, dlatent, dmean, dstd, dnorm, torch.float64)
+        arrs = {
+            "y0": y0.numpy(), "t": t.numpy(),
+            "dlatent": dlatent.numpy(), "dmean": dmean.numpy(), "dstd": dstd.numpy(),
+            "dnorm": np.array([dnorm]),
+        }
+        for k, v in sd32.items():
+            arrs["w_" + k] = v.numpy()
+        for k, v in o32.items():
+            if k in ("latent", "mean", "std", "fa_norm"):
+                arrs["ref32_" + k] = v.float().numpy()
+        for k, v in o64.items():
+            arrs["ref64_" + k] = v.double().numpy()
+        dist = {k: normwise_rel(o32[k], o64[k]) for k in o64}
+        meta = {
+            "name": name, "kind": kind, "n_regions": R, "latent_dim": L,
+            "net_sizes": net, "aug_net_sizes": aug, "n_traj": N,
+            "step": step, "fa_w": fa_w, "masked": masked,
+            "state_dict_keys": list(sd32.keys()),
+            "ref32_vs_ref64": dist,
+            "generator": "tests/golden/make_golden.py (reference lib/models.py + oracle RK4)",
+        }
+        arrs["meta_json"] = np.array(json.dumps(meta))
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **arrs)
+        worst = max(dist.values())
+        print(f"{name:22s} N={N:3d} T={len(t):3d} worst ref32-vs-ref64 rel={worst:.2e} -> {path}")
+
+    # single-eval RHS fixtures, including states on/over the mask boundary
+    torch.manual_seed(77)
+    gen = torch.Generator().manual_seed(78)
+    for kind in ("Fp", "Fa", "FaFp"):
+        for R in (1, 4):
+            mod = build_module(kind, R, 8, [16, 16, 8], [16, 12])
+            x = torch.randn(33, R, 8, generator=gen) * 1.2
+            x[0, 0, 0] = 2.0
+            x[1, 0, 1] = -1.0
+            x[2, 0, 2] = 2.0000002
+            x[3, 0, 0] = -1.0000001
+            mod.clear_tracking()
+            res = mod(0.0, x.clone())
+            arrs = {"x": x.numpy(), "res": res.detach().numpy()}
+            if kind != "Fa":
+                arrs["p"] = mod.params[0].detach().numpy()
+            if kind != "Fp":
+                arrs["fa"] = mod.tracker[0].detach().numpy()
+            for k, v in mod.state_dict().items():
+                arrs["w_" + k] = v.numpy()
+            meta = {"kind": kind, "n_regions": R, "latent_dim": 8, "net_sizes": [16, 16, 8],
+                    "aug_net_sizes": [16, 12], "state_dict_keys": list(mod.state_dict().keys())}
+            arrs["meta_json"] = np.array(json.dumps(meta))
+            np.savez_compressed(os.path.join(HERE, f"rhs_{kind.lower()}_r{R}.npz"), **arrs)
+    print("rhs fixtures written")
+
+
+if __name__ == "__main__":
+    main()

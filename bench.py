@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: fused RK4 solve of the SIR-UDE + VJP through it.
+
+Metric (BASELINE.json): UDE trajectories x steps / s (fwd+bwd), batch = states x
+seasons, whole job over all ranks.  One "step" = one forward solve of the
+trajectory batch (all RK4 steps, all 4 stages, outputs at every grid point) plus
+the VJP w.r.t. y0 and every RHS weight given d latent and d (posterior mean,
+std, |Fa|), plus -- with N > 1 ranks -- the side-statistic all-reduce and the
+parameter-gradient all-reduce (RCCL).
+
+Workload (per rank, weak scaling): BASELINE configs[1] "50 states x 10 seasons
+x 28-day windows": the reference's state model (run_ode.py:41-49, R = 49 regions
+flattened jointly into the FaFp MLPs, latent_dim 8, net [64,64,32], aug
+[64,64]) on 64 MC samples x 10 seasons x 32 windows = 20,480 trajectories, 8
+weekly RK4 steps (dt = 1 week, the longest training curriculum of run_ode.py
+:147-152, gamma = 56).  Synthetic inputs, default nn.Linear init, seed 0.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "forecasting-influenza-using-universal-differential-equations_amd"
+
+METRIC = "UDE trajectories×steps/sec (fwd+bwd), batch=states×seasons, at 1/2/4/8 MI355X"
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector == FP32 MFMA dense peak
+PEAK_HBM_GBS = 8000.0
+
+WORKLOADS = {
+    "state49": dict(kind="FaFp", R=49, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=64 * 10 * 32,
+                    t=("arange", 9, 1.0),
+                    desc="state model R=49 (joint), 64 MC samples x 10 seasons x 32 windows, 8 weekly RK4 steps"),
+    "us_northstar": dict(kind="FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=4096,
+                         t=("arange", 366, 7.0),
+                         desc="US model R=1, 4096 trajectories x 365 daily RK4 steps (north-star M1)"),
+}
+
+
+def macs_per_eval(w):
+    """Multiply-adds of one RHS evaluation with the full R*L layer-0 input."""
+    R, L = w["R"], w["L"]
+    tot = 0
+    for sizes, out in ((w["net"], 2 * R), (w["aug"], 3 * R)):
+        if sizes is None:
+            continue
+        dims = [R * L] + list(sizes) + [out]
+        tot += sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    return tot
+
+
+def make_t(spec):
+    kind, n, div = spec
+    return torch.arange(n, dtype=torch.float32) / div
+
+
+def synthetic_y0(gen, N, R, L):
+    S = torch.rand(N, R, generator=gen) * 0.4 + 0.5
+    I = torch.rand(N, R, generator=gen) * 0.05
+    rest = torch.randn(N, R, L - 3, generator=gen)
+    return torch.cat([S[..., None], I[..., None], (1 - S - I)[..., None], rest], -1) + 1e-5
+
+
+def build(pkg, w, device, seed):
+    torch.manual_seed(0)                         # identical weights on every rank
+    cls = getattr(pkg, w["kind"])
+    kw = {}
+    if w["net"] is not None:
+        kw["net_sizes"] = w["net"]
+    if w["aug"] is not None:
+        kw["aug_net_sizes"] = w["aug"]
+    mod = cls(w["R"], latent_dim=w["L"], **kw).to(device)
+    gen = torch.Generator().manual_seed(seed)
+    y0 = synthetic_y0(gen, w["n_traj"], w["R"], w["L"]).to(device).requires_grad_(True)
+    t = make_t(w["t"])
+    dlat = torch.randn((len(t),) + tuple(y0.shape), generator=gen).to(device)
+    return mod, y0, t, dlat
+
+
+def one_step(pkg, udist, mod, y0, t, dlat, world):
+    mod.clear_tracking()
+    mod.zero_grad(set_to_none=True)
+    y0.grad = None
+    latent = pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+    if world > 1:
+        udist.sync_side_stats(mod)
+    outs, cots = [latent], [dlat]
+    if mod.ode_type in ("Fp", "FaFp"):
+        post = mod.posterior()
+        outs += [post.loc, post.scale]
+        cots += [torch.tensor([0.3, -0.2], device=y0.device), torch.tensor([0.5, 0.1], device=y0.device)]
+    if mod.ode_type in ("Fa", "FaFp"):
+        outs.append(torch.norm(torch.stack(mod.tracker)))
+        cots.append(torch.tensor(0.1, device=y0.device))
+    torch.autograd.backward(outs, cots)
+    if world > 1:
+        udist.all_reduce_grads(mod.parameters())
+
+
+def time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier):
+    from ude_amd import fused
+    for _ in range(warmup):
+        one_step(pkg, udist, mod, y0, t, dlat, world)
+    torch.cuda.synchronize()
+    fused.EVENTS = []
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step(pkg, udist, mod, y0, t, dlat, world)
+    barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    evs = fused.EVENTS
+    fused.EVENTS = None
+    k_ms = {"fwd": [], "bwd": []}
+    for kind, e0, e1 in evs:
+        k_ms[kind].append(e0.elapsed_time(e1))
+    return el, {k: (sum(v) / len(v) if v else None) for k, v in k_ms.items()}
+
+
+def cpu_baseline(w, mod_gpu, budget_s=12.0):
+    """The oracle (PyTorch CPU restatement, fp32, autograd) on a bounded sample."""
+    from oracle.ude_oracle import OracleRHS, solve_and_grad
+    torch.set_num_threads(1)                     # the reference's own setting (run_ode.py:28)
+    rhs = OracleRHS.from_module(_cpu_copy(mod_gpu))
+    n = 1024 if w["R"] > 10 else 4096
+    steps_cap = 8 if w["R"] > 10 else 40
+    tt = make_t(w["t"])[: steps_cap + 1]
+    gen = torch.Generator().manual_seed(123)
+    y0 = synthetic_y0(gen, n, w["R"], w["L"])
+    dl = torch.randn((len(tt),) + tuple(y0.shape), generator=gen)
+    dm, ds = torch.tensor([0.3, -0.2]), torch.tensor([0.5, 0.1])
+    best = None
+    t_start = time.perf_counter()
+    reps = 0
+    while reps < 5 and (reps < 2 or time.perf_counter() - t_start < budget_s):
+        a = time.perf_counter()
+        solve_and_grad(rhs, y0, tt, tt[1] - tt[0], dl, dm, ds, 0.1)
+        d = time.perf_counter() - a
+        best = d if best is None else min(best, d)
+        reps += 1
+    units = n * (len(tt) - 1)
+    return {"value": units / best, "unit": "traj*steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ude_oracle.py (PyTorch CPU fp32 + autograd, torch.set_num_threads(1) as "
+                      f"run_ode.py:28) on {n} trajectories x {len(tt) - 1} steps of the same model, "
+                      f"fwd+bwd incl. posterior/|Fa| terms, best of {reps}",
+            "host_cpus": os.cpu_count()}
+
+
+def _cpu_copy(mod):
+    import copy
+    mod.clear_tracking()
+    return copy.deepcopy(mod).cpu()
+
+
+def read_pmc(name):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
+    p = os.path.join(REPO, "profiles", "pmc_" + name + ".json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="state49", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        barrier = lambda: dist.barrier()
+    else:
+        barrier = lambda: None
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    pkg = importlib.import_module(PKG)
+    from ude_amd import distributed as udist
+
+    w = WORKLOADS[args.workload]
+    mod, y0, t, dlat = build(pkg, w, dev, seed=1000 + rank)
+    el, kms = time_steps(pkg, udist, mod, y0, t, dlat, world, args.steps, args.warmup, barrier)
+    if world > 1:
+        x = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x)
+    n_steps_rk = len(t) - 1
+    units = world * w["n_traj"] * n_steps_rk * args.steps
+    value = units / el
+    macs = macs_per_eval(w)
+    flop_unit = 4 * 6 * macs                                  # fwd + dX + dW per traj*step
+    bwd_flop_launch = 4 * 4 * macs * w["n_traj"] * n_steps_rk  # dX + dW only (recompute not counted)
+    fwd_flop_launch = 4 * 2 * macs * w["n_traj"] * n_steps_rk
+
+    res = None
+    if rank == 0:
+        achieved = bwd_flop_launch / (kms["bwd"] * 1e-3) / 1e12 if kms["bwd"] else None
+        pmc = read_pmc(args.workload + "_bwd")
+        res = {
+            "metric": METRIC, "value": value, "unit": "traj*steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded y0 per SURVEY 8d, default nn.Linear init, N(0,1) d latent)",
+            "config": {"workload": args.workload, "description": w["desc"], "model": w["kind"],
+                       "n_regions": w["R"], "latent_dim": w["L"], "net_sizes": w["net"],
+                       "aug_net_sizes": w["aug"], "traj_per_gpu": w["n_traj"], "global_batch": world * w["n_traj"],
+                       "rk4_steps": n_steps_rk, "parallelism": f"dp{world}"},
+            "roofline": {"kernel": "ude_bwd_kernel (+ grad finalize)", "bound": "mfma",
+                         "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
+                         "traffic": pmc, "avg_launch_ms": kms["bwd"],
+                         "algorithmic_flop_per_launch": bwd_flop_launch},
+            "kernels": {"fwd_ms": kms["fwd"], "bwd_ms": kms["bwd"],
+                        "fwd_tflops": fwd_flop_launch / (kms["fwd"] * 1e-3) / 1e12 if kms["fwd"] else None,
+                        "step_tflops_algorithmic": value * flop_unit / 1e12,
+                        "rhs_evals_per_s": 4 * value},
+        }
+    if rank == 0 and world == 1 and not args.no_extra and args.workload == "state49":
+        w2 = WORKLOADS["us_northstar"]
+        m2, y2, t2, d2 = build(pkg, w2, dev, seed=7)
+        el2, k2 = time_steps(pkg, udist, m2, y2, t2, d2, 1, 3, 1, barrier)
+        v2 = w2["n_traj"] * (len(t2) - 1) * 3 / el2
+        res["north_star_M1"] = {"workload": "us_northstar", "description": w2["desc"],
+                                "traj_steps_per_s": v2, "rhs_evals_per_s": 4 * v2,
+                                "ms_per_step": el2 / 3 * 1e3, "fwd_ms": k2["fwd"], "bwd_ms": k2["bwd"],
+                                "target_rhs_evals_per_s": 1e7}
+        del m2, y2, d2
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(w, mod)
+    if rank == 0:
+        print(json.dumps(res))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""Data-parallel pieces of the hot path (one process per GPU, RCCL over xGMI).
+
+Trajectories are independent, so the batch shards along windows (SURVEY
+section 8e; keep all MC samples of a window on one rank so the per-window
+sample statistics of ``nll_loss`` stay local).  Two exchanges are real:
+
+1. forward: the posterior over *all* recorded rates and the Fa norm are
+   global (lib/models.py:152-156, lib/VAE.py:180).  Each rank's fused solve
+   yields (mean, std, |Fa|) over its shard; ``sync_side_stats`` turns them into
+   sufficient statistics (n*mean, (n-1)*std^2 + n*mean^2, |Fa|^2), all-reduces
+   those 5 numbers and rebuilds the global (mean, std, |Fa|).  The all-reduce
+   is differentiable (its backward all-reduces the cotangent), so every rank's
+   kernel receives d loss_total / d stats in its backward.
+2. backward: one bucketed all-reduce of the flat parameter gradients.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List
+
+import torch
+import torch.distributed as dist
+
+
+class _AllReduceSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = x.clone()
+        dist.all_reduce(y, op=dist.ReduceOp.SUM)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.clone()
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        return g
+
+
+def all_reduce_sum(x: torch.Tensor) -> torch.Tensor:
+    """Differentiable SUM all-reduce (identity when not distributed)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    return _AllReduceSum.apply(x)
+
+
+def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: torch.Tensor):
+    """Global (n, mean, std, norm) from per-rank values (Chan's pooled variance, fp64)."""
+    n = torch.tensor([n_local], dtype=torch.float64, device=mean.device)
+    m = mean.double()
+    s = std.double()
+    suff = torch.cat([n, n * m, (n - 1.0) * s * s + n * m * m, norm.double().reshape(1) ** 2])
+    tot = all_reduce_sum(suff)
+    n_tot = tot[0]
+    gmean = tot[1:3] / n_tot
+    gvar = (tot[3:5] - n_tot * gmean * gmean) / (n_tot - 1.0)
+    gstd = torch.sqrt(torch.clamp(gvar, min=0.0))
+    gnorm = torch.sqrt(tot[5:6])
+    return n_tot, gmean.to(mean.dtype), gstd.to(std.dtype), gnorm.to(norm.dtype)
+
+
+def sync_side_stats(module) -> None:
+    """Replace the module's recorded fused-solve statistics by their global values."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    rates = list(module._fused_rates)
+    tracker = list(module.tracker)
+    if not rates and not tracker:
+        return
+    if rates:
+        n, m, s = rates[-1]
+    else:
+        n, m, s = 1.0, torch.zeros(2, device=tracker[-1].device), torch.ones(2, device=tracker[-1].device)
+    norm = tracker[-1] if tracker else torch.zeros(1, device=m.device)
+    n_tot, gm, gs, gn = combine_stats(n, m, s, norm)
+    if rates:
+        module._fused_rates[-1] = (n_tot, gm, gs)
+    if tracker:
+        module.tracker[-1] = gn
+
+
+def all_reduce_grads(params: Iterable[torch.nn.Parameter], average: bool = True) -> None:
+    """One flat bucket (the ODE has <= ~0.3 MB of gradients: a single ring all-reduce)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    ps: List[torch.nn.Parameter] = [p for p in params if p.grad is not None]
+    if not ps:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    if average:
+        flat /= dist.get_world_size()
+    off = 0
+    for p in ps:
+        n = p.grad.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n

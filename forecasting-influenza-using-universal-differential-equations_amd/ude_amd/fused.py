@@ -44,6 +44,16 @@ def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.d
     return Plan(lib, desc, prob, sizes, sched, schedule.n_times, n_eval, param_shapes)
 
 
+# Optional HIP-event instrumentation (bench.py): when a list, every forward /
+# backward C-ABI call appends (kind, start_event, end_event) recorded on the
+# stream the kernels are launched on.
+EVENTS = None
+
+
+def _ev(dev):
+    return torch.cuda.Event(enable_timing=True)
+
+
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -67,8 +77,12 @@ class FusedRK4(torch.autograd.Function):
         ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) if need_grad else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
         stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
         plan.lib.forward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
                          latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), stats.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
         ctx.plan = plan
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
@@ -87,9 +101,13 @@ class FusedRK4(torch.autograd.Function):
         dy0 = torch.empty_like(y0)
         slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
         dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
         plan.lib.backward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
                           ckpt.data_ptr(), dlatent.data_ptr(), stats.data_ptr(), dstats.data_ptr(),
                           dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         grads = []
         off = 0
         for shp in plan.param_shapes:

@@ -4,8 +4,8 @@ import torch
 
 
 def normwise_rel(a, b):
-    a = torch.as_tensor(a).double().cpu()
-    b = torch.as_tensor(b).double().cpu()
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
     den = max(float(torch.linalg.vector_norm(b)), 1e-30)
     return float(torch.linalg.vector_norm(a - b)) / den
 

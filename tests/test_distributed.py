@@ -1,0 +1,74 @@
+"""Data-parallel exchange steps on a gloo/CPU group (world_size 2).
+
+The posterior statistics and |Fa| are global over every rank's trajectories
+(lib/models.py:152-156, lib/VAE.py:180); ude_amd.distributed.combine_stats
+all-reduces their sufficient statistics differentiably.  Checked against the
+single-process values and gradients of the same data.
+"""
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO, import_pkg
+
+WORLD = 2
+
+
+def _worker(rank, port, q):
+    try:
+        sys.path.insert(0, REPO)
+        import_pkg()
+        from ude_amd import distributed as udist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        gen = torch.Generator().manual_seed(11)
+        p_all = torch.rand(300, 2, generator=gen, dtype=torch.float64) + 0.1
+        fa_all = torch.randn(300, 3, generator=gen, dtype=torch.float64)
+        lo, hi = (0, 180) if rank == 0 else (180, 300)      # uneven shards
+        p = p_all[lo:hi].clone().requires_grad_(True)
+        fa = fa_all[lo:hi].clone().requires_grad_(True)
+        n_tot, m, s, nrm = udist.combine_stats(float(hi - lo), p.mean(0), p.std(0), torch.norm(fa))
+        # every rank computes the same global loss term; grads of the SUM over ranks
+        loss = (m * torch.tensor([0.3, -0.2], dtype=torch.float64)).sum() \
+            + (s * torch.tensor([0.5, 0.1], dtype=torch.float64)).sum() + 0.1 * nrm.sum()
+        loss.backward()
+        gp = p.grad.clone()
+        gf = fa.grad.clone()
+        # gradient averaging across ranks as in all_reduce_grads: grads here are per-rank
+        # contributions d(sum_r loss_r)/d p_local, which must equal WORLD x the single-process grad
+        q.put((rank, float(n_tot), m.detach(), s.detach(), nrm.detach(), gp, gf, lo, hi))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+
+
+def test_combine_stats_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] != "err" for r in res), res
+    gen = torch.Generator().manual_seed(11)
+    p_all = (torch.rand(300, 2, generator=gen, dtype=torch.float64) + 0.1).requires_grad_(True)
+    fa_all = torch.randn(300, 3, generator=gen, dtype=torch.float64).requires_grad_(True)
+    m, s, nrm = p_all.mean(0), p_all.std(0), torch.norm(fa_all)
+    loss = (m * torch.tensor([0.3, -0.2], dtype=torch.float64)).sum() \
+        + (s * torch.tensor([0.5, 0.1], dtype=torch.float64)).sum() + 0.1 * nrm
+    loss.backward()
+    for rank, n_tot, rm, rs, rn, gp, gf, lo, hi in res:
+        assert n_tot == 300
+        assert torch.allclose(rm, m.detach()) and torch.allclose(rs, s.detach())
+        assert torch.allclose(rn, nrm.detach().reshape(1))
+        assert torch.allclose(gp, WORLD * p_all.grad[lo:hi])
+        assert torch.allclose(gf, WORLD * fa_all.grad[lo:hi])

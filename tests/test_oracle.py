@@ -1,0 +1,147 @@
+"""The CPU oracle is pinned before it is trusted.
+
+1. Against the golden vectors made from the reference's own RHS classes
+   (tests/golden/make_golden.py): single evaluations (rhs_*.npz) and whole
+   solves + VJPs (fp64).
+2. Against analytic known answers for the integrator (torchdiffeq RK4 is not
+   available to pin it): constant-rate SIR vs scipy solve_ivp, the 4th-order
+   convergence rate, a linear ODE vs expm, and the output-interpolation rule.
+"""
+import numpy as np
+import pytest
+import scipy.integrate
+import scipy.linalg
+import torch
+
+from conftest import load_golden, rhs_cases, solver_cases
+from helpers import normwise_rel, step_of
+from oracle.ude_oracle import (OracleRHS, make_grid, odeint_rk4, output_schedule, solve_and_grad)
+
+
+def oracle_from_golden(g, dtype=torch.float64):
+    m = g["meta"]
+    o = OracleRHS(kind=m["kind"], n_regions=m["n_regions"], latent_dim=m["latent_dim"])
+    keys = m["state_dict_keys"]
+    W = {k[:-len(".weight")]: torch.from_numpy(g["w_" + k]).to(dtype) for k in keys if k.endswith(".weight")}
+    B = {k[:-len(".bias")]: torch.from_numpy(g["w_" + k]).to(dtype) for k in keys if k.endswith(".bias")}
+
+    def layers(prefix):
+        names = sorted((n for n in W if n.startswith(prefix + ".")), key=lambda n: int(n.split(".")[1]))
+        k = len(names) - 1
+        return [W[n] for n in names], [B[n] for n in names], [i < k - 1 for i in range(len(names))]
+
+    if m["kind"] in ("Fp", "FaFp"):
+        o.p_w, o.p_b, o.p_act = layers("net" if m["kind"] == "FaFp" else "Fp_net")
+    if m["kind"] in ("Fa", "FaFp"):
+        o.a_w, o.a_b, o.a_act = layers("aug_net")
+    o.fa_w = float(m.get("fa_w", 1.0))
+    return o
+
+
+@pytest.mark.parametrize("case", rhs_cases())
+def test_oracle_rhs_matches_reference_eval(case):
+    g = load_golden(case)
+    o = oracle_from_golden(g, torch.float32)
+    x = torch.from_numpy(g["x"])
+    res = o(0.0, x)
+    assert torch.allclose(res, torch.from_numpy(g["res"]), rtol=1e-6, atol=1e-7)
+    if "p" in g:
+        assert torch.allclose(o.params[0], torch.from_numpy(g["p"]), rtol=1e-6, atol=1e-7)
+    if "fa" in g:
+        assert torch.allclose(o.tracker[0], torch.from_numpy(g["fa"]), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("case", solver_cases())
+def test_oracle_solve_matches_golden_fp64(case):
+    g = load_golden(case)
+    o = oracle_from_golden(g, torch.float64)
+    t, h = step_of(g)
+    r = solve_and_grad(o, torch.from_numpy(g["y0"]).double(), t, h, torch.from_numpy(g["dlatent"]),
+                       torch.from_numpy(g["dmean"]), torch.from_numpy(g["dstd"]), float(g["dnorm"][0]))
+    assert normwise_rel(r.latent, g["ref64_latent"]) < 1e-12
+    if r.mean is not None:
+        assert normwise_rel(r.mean, g["ref64_mean"]) < 1e-12
+        assert normwise_rel(r.std, g["ref64_std"]) < 1e-12
+    if r.fa_norm is not None:
+        assert normwise_rel(r.fa_norm, g["ref64_fa_norm"]) < 1e-12
+    assert normwise_rel(r.grads["y0"], g["ref64_d_y0"]) < 1e-11
+    # every weight gradient: oracle names p_w{i}/p_b{i}/a_w{i}/a_b{i} vs state_dict order
+    keys = g["meta"]["state_dict_keys"]
+    names = [n for n in r.grads if n != "y0"]
+    assert len(names) == len(keys)
+    for n, k in zip(names, keys):
+        assert normwise_rel(r.grads[n], g["ref64_d_" + k]) < 1e-10, (n, k)
+
+
+def _const_rate_sir(beta, gamma):
+    o = OracleRHS(kind="Fp", n_regions=1, latent_dim=3)
+    w1 = torch.zeros(4, 3, dtype=torch.float64)
+    w2 = torch.zeros(2, 4, dtype=torch.float64)
+    o.p_w = [w1, w2]
+    o.p_b = [torch.zeros(4, dtype=torch.float64), torch.tensor([beta, -gamma], dtype=torch.float64)]
+    o.p_act = [False, False]
+    return o
+
+
+def _sir_exact(beta, gamma, y0, t_end):
+    f = lambda t, y: [-beta * y[0] * y[1], beta * y[0] * y[1] - gamma * y[1], gamma * y[1]]
+    s = scipy.integrate.solve_ivp(f, (0, t_end), y0, rtol=1e-12, atol=1e-14, method="DOP853")
+    return s.y[:, -1]
+
+
+def test_constant_rate_sir_vs_solve_ivp():
+    beta, gamma = 0.9, 0.35
+    o = _const_rate_sir(beta, gamma)
+    y0 = torch.tensor([[[0.8, 0.05, 0.15]]], dtype=torch.float64)
+    t = torch.linspace(0, 10, 201, dtype=torch.float64)
+    lat = odeint_rk4(o, y0, t, None)
+    exact = _sir_exact(beta, gamma, [0.8, 0.05, 0.15], 10.0)
+    assert np.abs(lat[-1, 0, 0].numpy() - exact).max() < 1e-7
+    # S + I + R is conserved by the flux
+    assert abs(float(lat[-1].sum()) - 1.0) < 1e-12
+
+
+def test_rk4_fourth_order_convergence():
+    beta, gamma = 1.3, 0.4
+    o = _const_rate_sir(beta, gamma)
+    y0 = torch.tensor([[[0.7, 0.1, 0.2]]], dtype=torch.float64)
+    exact = _sir_exact(beta, gamma, [0.7, 0.1, 0.2], 8.0)
+    errs = []
+    for n in (20, 40, 80):
+        t = torch.linspace(0, 8, n + 1, dtype=torch.float64)
+        errs.append(np.abs(odeint_rk4(o, y0, t, None)[-1, 0, 0].numpy() - exact).max())
+    r1, r2 = errs[0] / errs[1], errs[1] / errs[2]
+    assert 12 < r1 < 20 and 12 < r2 < 20, errs
+
+
+def test_linear_ode_vs_expm():
+    gen = torch.Generator().manual_seed(0)
+    A = torch.randn(4, 4, generator=gen, dtype=torch.float64) * 0.5
+    x0 = torch.randn(3, 4, generator=gen, dtype=torch.float64)
+    t = torch.linspace(0, 2, 401, dtype=torch.float64)
+    sol = odeint_rk4(lambda tt, x: x @ A.T, x0, t, None)
+    ref = x0 @ torch.from_numpy(scipy.linalg.expm(2.0 * A.numpy())).T
+    assert float((sol[-1] - ref).abs().max()) < 1e-9
+
+
+def test_step_size_grid_and_interpolation_rule():
+    # tuning/tune_encoders.py:132/:221 pattern: daily outputs, weekly steps
+    t = torch.linspace(1, 20, 20) / 7
+    grid = make_grid(t, 1.0)
+    assert grid[0] == t[0] and grid[-1] == t[-1]
+    assert len(grid) == int(np.ceil((float(t[-1]) - float(t[0])) / 1.0 + 1))
+    sched = output_schedule(t, grid)
+    assert [s[0] for s in sched] == list(range(1, 20))
+    modes = {s[2] for s in sched}
+    assert 2 in modes                                        # interpolated outputs exist
+    # linear interpolation of y = t is exact
+    lat = odeint_rk4(lambda tt, x: torch.ones_like(x), torch.zeros(1, 1, dtype=torch.float64),
+                     t.double(), 1.0)
+    assert float((lat[:, 0, 0] - (t.double() - t[0].double())).abs().max()) < 1e-6
+
+
+def test_daily_grids_have_no_spurious_points():
+    # t = arange(n)/7 with h = t[1]-t[0] gives exactly len(t) grid points
+    for n in (2, 9, 29, 57, 85, 366):
+        t = torch.arange(n, dtype=torch.float32) / 7
+        assert len(make_grid(t, t[1] - t[0])) == n

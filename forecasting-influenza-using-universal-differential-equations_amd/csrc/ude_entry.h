@@ -8,6 +8,10 @@
 
 namespace ude {
 
+#ifdef UDE_PROFILE
+extern unsigned long long* g_prof_buffer;   // diagnostic builds: set by ude_debug_set_prof()
+#endif
+
 template <class M>
 bool matches(const UdeModelDesc* d) {
   if (d->kind != M::KIND || d->n_regions != M::R || d->latent_dim != M::L) return false;
@@ -138,6 +142,9 @@ struct Ops {
     a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
     a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.stats_out = stats_out; a.dstats = dstats;
     a.dy0 = dy0; a.slab = slab;
+#ifdef UDE_PROFILE
+    a.prof = g_prof_buffer;
+#endif
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
     hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);

@@ -61,7 +61,30 @@ struct KArgs {
   float* slab;
   int n_traj, n_steps, n_out, n_tiles;
   float fa_w;
+  unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
 };
+
+// In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
+// s_memtime deltas accumulated per segment; compiled out otherwise.
+constexpr int NPROF = 16;
+struct Prof {
+  unsigned long long acc[NPROF];
+  unsigned long long last;
+};
+#ifdef UDE_PROFILE
+#define UDE_STAMP(pf, seg)                                                    \
+  do {                                                                        \
+    if (pf) {                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                      \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();             \
+      __builtin_amdgcn_sched_barrier(0);                                      \
+      (pf)->acc[seg] += t_ - (pf)->last;                                      \
+      (pf)->last = t_;                                                        \
+    }                                                                         \
+  } while (0)
+#else
+#define UDE_STAMP(pf, seg) do { } while (0)
+#endif
 
 struct Sched {
   const float* dt;
@@ -78,18 +101,29 @@ struct Sched {
   }
 };
 
+// Packed weights are read through a buffer resource (SGPR descriptor): every
+// fragment load is `voffset = lane*16` + a compile-time scalar offset, so no
+// per-tile 64-bit lane addresses are materialised (they were hoisted out of the
+// step loop and spilled).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 ldw(Rsrc rs, int voff_bytes, int soff_bytes) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff_bytes, soff_bytes, 0));
+}
+
 // One 16-row tile of  C[o][t] += sum_k A[o][k] * B[t][k]  with K = KP (multiple of 16).
-// A: packed fragments in global memory ([KP/16][64][4] for this tile);
+// A: packed fragments at float offset WOFF of the pack ([KP/16][64][4] for this tile);
 // B: the per-trajectory LDS record, lane group g reading features [g*KP/4, (g+1)*KP/4).
-template <int KP>
-__device__ __forceinline__ f4 gemm_tile(const float* __restrict__ wp, const float* bp, int lane, f4 acc) {
+template <int KP, int WOFF>
+__device__ __forceinline__ f4 gemm_tile(Rsrc rs, const float* bp, int lane, f4 acc) {
   constexpr int KQ = KP / 4;
   constexpr int NQ = KP / 16;
-  const f4* w = reinterpret_cast<const f4*>(wp) + lane;
   const float* b = bp + (lane >> 4) * KQ;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const f4 a = w[q * 64];
+    const f4 a = ldw(rs, lane * 16, (WOFF + q * 256) * 4);
     const f4 x = *reinterpret_cast<const f4*>(b + 4 * q);
     acc = mfma4(a[0], x[0], acc);
     acc = mfma4(a[1], x[1], acc);
@@ -108,8 +142,7 @@ using C1Arr = f4[NZ_ > 0 ? NZ_ : 1];
 // Leaves post-activation outputs of every layer in the record (the final
 // layers' raw outputs: P-net pre-|.| rates q, A-net Fa).  Ends on a barrier.
 template <class M, int W, int SR>
-__device__ __forceinline__ void mlp_forward(const float* __restrict__ pack, float* lds,
-                                            const f4* c1, int lane) {
+__device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, int lane, Prof* pf = nullptr) {
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto dd) {
@@ -125,23 +158,25 @@ __device__ __forceinline__ void mlp_forward(const float* __restrict__ pack, floa
         if constexpr (d == 0 && M::S > 0) {
           acc = c1[M::nz_before(W, k)];
         } else {
-          acc = *reinterpret_cast<const f4*>(pack + M::b_off(net, d) + rt * 16 + g * 4);
+          acc = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
         }
-        acc = gemm_tile<KP>(pack + M::wf_off(net, d) + rt * (KP / 16) * 256, rec + inoff, lane, acc);
+        acc = gemm_tile<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, rec + inoff, lane, acc);
         if constexpr (M::act(net, d)) {
           acc[0] = elu1(acc[0]); acc[1] = elu1(acc[1]);
           acc[2] = elu1(acc[2]); acc[3] = elu1(acc[3]);
         }
         *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = acc;
+        __builtin_amdgcn_sched_barrier(0);   // bound live ranges: one tile's fragments at a time
       }
     });
     __syncthreads();
+    UDE_STAMP(pf, 2 + d);
   });
 }
 
 // Static-feature hoist: c1[o][t] = b0[o] + sum_s W0[o][static s] * x_static[t][s].
 template <class M, int W, int SR, int XOFF>
-__device__ __forceinline__ void static_hoist(const float* __restrict__ pack, const float* lds, f4* c1, int lane) {
+__device__ __forceinline__ void static_hoist(Rsrc rs, const float* lds, f4* c1, int lane) {
   if constexpr (M::S > 0) {
     const int t = lane & 15, g = lane >> 4;
     sfor<M::FT(0)>([&](auto kk) {
@@ -149,8 +184,8 @@ __device__ __forceinline__ void static_hoist(const float* __restrict__ pack, con
       if constexpr (M::fowner(0, k) == W) {
         constexpr int net = M::fnet(0, k);
         constexpr int rt = M::frt(0, k);
-        f4 acc = *reinterpret_cast<const f4*>(pack + M::b_off(net, 0) + rt * 16 + g * 4);
-        acc = gemm_tile<M::S16>(pack + M::wsf_off(net) + rt * (M::S16 / 16) * 256, lds + t * SR + XOFF, lane, acc);
+        f4 acc = ldw(rs, g * 16, (M::b_off(net, 0) + rt * 16) * 4);
+        acc = gemm_tile<M::S16, M::wsf_off(net) + rt * (M::S16 / 16) * 256>(rs, lds + t * SR + XOFF, lane, acc);
         c1[M::nz_before(W, k)] = acc;
       }
     });
@@ -161,6 +196,7 @@ __device__ __forceinline__ void static_hoist(const float* __restrict__ pack, con
 template <class M, int SR, int XOFF>
 __device__ __forceinline__ void load_static(const float* __restrict__ y0, float* lds, int n0, int n_traj) {
   if constexpr (M::S > 0) {
+    #pragma unroll 1
     for (int i = threadIdx.x; i < TT * M::S16; i += NTHREADS) {
       const int t = i / M::S16, s = i - t * M::S16;
       const int n = n0 + t;
@@ -194,8 +230,10 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63;
   const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
   double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
 
+  #pragma unroll 1
   for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
   __syncthreads();
 
@@ -227,13 +265,13 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
     __syncthreads();
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
-    static_hoist<M, W, SR, M::XSF_OFF>(A.pack, lds, c1, lane);
+    static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
     __syncthreads();
 
     for (int step = 0; step < A.n_steps; ++step) {
       const float dt = sc.dt[step];
       for (int j = 0; j < 4; ++j) {
-        mlp_forward<M, W, SR>(A.pack, lds, c1, lane);
+        mlp_forward<M, W, SR>(rs, lds, c1, lane);
         sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
@@ -289,6 +327,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
               }
               if (valid) {
                 const int o_end = sc.out_start[step + 1];
+                #pragma unroll 1
                 for (int o = sc.out_start[step]; o < o_end; ++o) {
                   const int jo = sc.out_j[o], mode = sc.out_mode[o];
                   const float slope = sc.out_slope[o];
@@ -353,9 +392,8 @@ __global__ __launch_bounds__(NTHREADS) void ude_fwd_kernel(KArgs a) {
 // ============================================================================
 // Backward (VJP)
 // ============================================================================
-template <class M, int W, int SR, class DW, class GA, class G0>
-__device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, float* lds,
-                                             DW& dw, GA& gacc, G0& g0t, int lane) {
+template <class M, int W, int SR, class DW, class G0>
+__device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0t, int lane, Prof* pf = nullptr) {
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
@@ -369,8 +407,22 @@ __device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, flo
         constexpr int goff = M::gbuf(net, d);
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
         const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
-        if constexpr (d == 0) g0t[M::nz_before(W, k)] += gv;
-        else gacc[M::ng_before(W, d, k)] += gv;
+        if constexpr (d == 0) {
+          g0t[M::nz_before(W, k)] += gv;          // per-trajectory sums: static-feature gradients
+        } else {
+          // bias gradient: sum over the tile's 16 trajectories, then into this
+          // wave's rows of the workgroup's LDS row sums (fixed order: deterministic)
+          f4 r = gv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+            r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+          }
+          if (t == 0) {
+            float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
+            db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+          }
+        }
         float ga[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
@@ -382,6 +434,7 @@ __device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, flo
           for (int s = 0; s < 4; ++s) acc = mfma4(ga[s], lds[(4 * g + s) * SR + inoff + ct * 16 + t], acc);
           dw[idx] = acc;
         });
+        __builtin_amdgcn_sched_barrier(0);
       }
     });
     // (2) gradient w.r.t. the layer input (rows = input features)
@@ -391,17 +444,17 @@ __device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, flo
         if constexpr (d == 0) {
           f4 acc = f4zero();
           if constexpr (M::HAS_P)
-            acc = gemm_tile<M::kout(0, 0)>(pack + M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256,
-                                           rec + M::gbuf(0, 0), lane, acc);
+            acc = gemm_tile<M::kout(0, 0), M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256>(
+                rs, rec + M::gbuf(0, 0), lane, acc);
           if constexpr (M::HAS_A)
-            acc = gemm_tile<M::kout(1, 0)>(pack + M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256,
-                                           rec + M::gbuf(1, 0), lane, acc);
+            acc = gemm_tile<M::kout(1, 0), M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256>(
+                rs, rec + M::gbuf(1, 0), lane, acc);
           *reinterpret_cast<f4*>(rec + M::GY_OFF + m * 16 + g * 4) = acc;
         } else {
           constexpr int net = M::xnet(d, m);
           constexpr int rt = M::xrt(d, m);
-          f4 acc = gemm_tile<M::kout(net, d)>(pack + M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256,
-                                              rec + M::gbuf(net, d), lane, f4zero());
+          f4 acc = gemm_tile<M::kout(net, d), M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256>(
+              rs, rec + M::gbuf(net, d), lane, f4zero());
           if constexpr (M::act(net, d - 1)) {
             const f4 av = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
 #pragma unroll
@@ -409,9 +462,11 @@ __device__ __forceinline__ void mlp_backward(const float* __restrict__ pack, flo
           }
           *reinterpret_cast<f4*>(rec + M::gbuf(net, d - 1) + rt * 16 + g * 4) = acc;
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     });
     __syncthreads();
+    UDE_STAMP(pf, 7 + d);
   });
 }
 
@@ -420,13 +475,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_B;
   constexpr int SL = M::SLOTS;
   constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
-  constexpr int NGn = M::NG(W) > 0 ? M::NG(W) : 1;
   constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int t16 = lane & 15, g = lane >> 4;
   const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_TOTAL;
+  const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
 
   // side-statistic cotangents -> per-eval gradient coefficients
   //   d mean_c / d p = 1/n ;  d std_c / d p = (p - mean_c) / ((n - 1) std_c)   (torch std backward)
@@ -447,134 +502,171 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
   }
 
-  f4 dw[NDWn], gacc[NGn], g0t[NZn], c1[NZn];
+  f4 dw[NDWn], g0t[NZn], c1[NZn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
-#pragma unroll
-  for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
+  Prof prof_, *pf = nullptr;
+#ifdef UDE_PROFILE
+  if (A.prof && tid == 0) {
+    pf = &prof_;
+    for (int i = 0; i < NPROF; ++i) prof_.acc[i] = 0;
+    prof_.last = __builtin_amdgcn_s_memtime();
+  }
+#endif
 
+  #pragma unroll 1
   for (int i = tid; i < M::SLAB_DB - M::SLAB_STATIC; i += NTHREADS) myslab[M::SLAB_STATIC + i] = 0.f;
-  for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
+  #pragma unroll 1
+  for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;
   __syncthreads();
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
     load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    #pragma unroll 1
+    for (int i = tid; i < TT * M::F; i += NTHREADS) {
+      const int t = i / M::F;
+      lds[t * SR + M::RK_A + (i - t * M::F)] = 0.f;
+    }
     __syncthreads();
-    static_hoist<M, W, SR, M::XSB_OFF>(A.pack, lds, c1, lane);
+    static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     __syncthreads();
 
-    float a[SL][3];
-#pragma unroll
-    for (int sl = 0; sl < SL; ++sl) a[sl][0] = a[sl][1] = a[sl][2] = 0.f;
-
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
-      float pend[SL][3], accy[SL][3], sdk[SL][3], dk1[SL][3], dk2[SL][3], dk3[SL][3], dyf[SL][2];
+      const int o_beg = sc.out_start[step], o_end = sc.out_start[step + 1];
+      // d latent of the outputs written after this step -> adjoint of y_{n+1} / y_n;
+      // then the stage cotangents of the 3/8 combination dy = (k1+3(k2+k3)+k4)*dt/8.
+      // (slots unrolled: every cotangent load of the step is in flight at once)
       sfor<SL>([&](auto ss) {
         constexpr int sl = decltype(ss)::value;
         const int p = tid + sl * NTHREADS;
-        pend[sl][0] = pend[sl][1] = pend[sl][2] = 0.f;
         if (p < M::PAIRS) {
           const int r = p / TT, t = p - r * TT;
           const int n = n0 + t;
+          float* rec = lds + t * SR;
+          float a[3], pend[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 3; ++c) a[c] = rec[M::RK_A + 3 * r + c];
           if (n < A.n_traj) {
-            const int o_end = sc.out_start[step + 1];
-            for (int o = sc.out_start[step]; o < o_end; ++o) {
-              const int jo = sc.out_j[o], mode = sc.out_mode[o];
+            #pragma unroll 1
+            for (int o = o_beg; o < o_end; ++o) {
+              const int mode = sc.out_mode[o];
               const float slope = sc.out_slope[o];
-              const float* gl = A.dlatent + (size_t)jo * NRL + ((size_t)n * M::R + r) * M::L;
+              const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL + ((size_t)n * M::R + r) * M::L;
 #pragma unroll
               for (int c = 0; c < 3; ++c) {
-                // y1-side / y0-side shares of d latent[jo] (torchdiffeq _linear_interp)
+                // y1-side / y0-side shares (torchdiffeq _linear_interp)
                 const float gv = gl[c];
                 const float sg = mode == 2 ? slope * gv : (mode == 1 ? gv : 0.f);
                 const float pg = mode == 2 ? gv - sg : (mode == 0 ? gv : 0.f);
-                a[sl][c] += sg;
-                pend[sl][c] += pg;
+                a[c] += sg;
+                pend[c] += pg;
               }
             }
           }
-        }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const float s = (a[sl][c] * 0.125f) * dt;
-          sdk[sl][c] = s; dk1[sl][c] = s; dk2[sl][c] = 3.0f * s; dk3[sl][c] = 3.0f * s;
-          accy[sl][c] = a[sl][c];
+          for (int c = 0; c < 3; ++c) {
+            const int f = 3 * r + c;
+            const float sdk = (a[c] * 0.125f) * dt;
+            rec[M::RK_A + f] = a[c];
+            rec[M::RK_PEND + f] = pend[c];
+            rec[M::RK_ACCY + f] = a[c];
+            rec[M::RK_DK1 + f] = sdk;
+            rec[M::RK_DK2 + f] = 3.0f * sdk;
+            rec[M::RK_DK3 + f] = 3.0f * sdk;
+          }
         }
       });
+      __builtin_amdgcn_sched_barrier(0);
 
       for (int jj = 3; jj >= 0; --jj) {
-        // stage input from the forward's checkpoint
-        sfor<SL>([&](auto ss) {
-          constexpr int sl = decltype(ss)::value;
-          const int p = tid + sl * NTHREADS;
-          if (p < M::PAIRS) {
+        // stage input from the forward's checkpoint (one SGPR descriptor per stage,
+        // all slots' loads issued before the first LDS store)
+        {
+          const Rsrc rck = make_rsrc(A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0), M::F * TT * 4);
+          float ck[SL][3];
+          sfor<SL>([&](auto ss) {
+            constexpr int sl = decltype(ss)::value;
+            const int p = tid + sl * NTHREADS;
             const int r = p / TT, t = p - r * TT;
+            const int v = (p < M::PAIRS) ? (3 * r * TT + t) * 4 : 0;
 #pragma unroll
             for (int c = 0; c < 3; ++c)
-              lds[t * SR + M::Y_OFF + 3 * r + c] = A.ckpt[ckpt_index(tile, A.n_steps, step, jj, M::F, 3 * r + c, t)];
-          }
-        });
+              ck[sl][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rck, v, c * TT * 4, 0));
+          });
+          sfor<SL>([&](auto ss) {
+            constexpr int sl = decltype(ss)::value;
+            const int p = tid + sl * NTHREADS;
+            if (p < M::PAIRS) {
+              const int r = p / TT, t = p - r * TT;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = ck[sl][c];
+            }
+          });
+        }
+        UDE_STAMP(pf, 0);
         __syncthreads();
-        mlp_forward<M, W, SR>(A.pack, lds, c1, lane);
+        UDE_STAMP(pf, 1);
+        mlp_forward<M, W, SR>(rs, lds, c1, lane, pf);
 
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y
-        sfor<SL>([&](auto ss) {
-          constexpr int sl = decltype(ss)::value;
-          const int p = tid + sl * NTHREADS;
-          dyf[sl][0] = dyf[sl][1] = 0.f;
-          if (p < M::PAIRS) {
-            const int r = p / TT, t = p - r * TT;
-            const bool valid = n0 + t < A.n_traj;
-            float* rec = lds + t * SR;
-            float Y[3], dres[3];
+        #pragma unroll 1
+        for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+          const int r = p / TT, t = p - r * TT;
+          const bool valid = n0 + t < A.n_traj;
+          float* rec = lds + t * SR;
+          float Y[3], dres[3];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const int f = 3 * r + c;
+            Y[c] = rec[M::Y_OFF + f];
+            const float dk = jj == 3 ? (rec[M::RK_A + f] * 0.125f) * dt
+                           : rec[(jj == 2 ? M::RK_DK3 : jj == 1 ? M::RK_DK2 : M::RK_DK1) + f];
+            dres[c] = (!valid || Y[c] > 2.f || Y[c] < -1.f) ? 0.f : dk;
+          }
+          if constexpr (M::HAS_A) {
+            constexpr int fo = M::act_off(1, M::nl(1) - 1);
+            constexpr int go = M::gbuf(1, M::nl(1) - 1);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-              Y[c] = rec[M::Y_OFF + 3 * r + c];
-              const float dk = jj == 3 ? sdk[sl][c] : jj == 2 ? dk3[sl][c] : jj == 1 ? dk2[sl][c] : dk1[sl][c];
-              dres[c] = (!valid || Y[c] > 2.f || Y[c] < -1.f) ? 0.f : dk;
-            }
-            if constexpr (M::HAS_A) {
-              constexpr int fo = M::act_off(1, M::nl(1) - 1);
-              constexpr int go = M::gbuf(1, M::nl(1) - 1);
-#pragma unroll
-              for (int c = 0; c < 3; ++c) {
-                const float fa = rec[fo + 3 * r + c];
-                float dfa = M::HAS_P ? A.fa_w * dres[c] : dres[c];
-                dfa = valid ? dfa + cn * fa : 0.f;
-                rec[go + 3 * r + c] = dfa;
-              }
-            }
-            if constexpr (M::HAS_P) {
-              constexpr int qo = M::act_off(0, M::nl(0) - 1);
-              constexpr int go = M::gbuf(0, M::nl(0) - 1);
-              const float q0 = rec[qo + 2 * r], q1 = rec[qo + 2 * r + 1];
-              const float b = fabsf(q0), gm = fabsf(q1);
-              const float dplus = dres[1] - dres[0];
-              const float dminus = dres[2] - dres[1];
-              const float dpi = dplus * Y[1];                 // d(beta*S)
-              float dbeta = dpi * Y[0];
-              const float dS = dpi * b;
-              const float dI = dplus * (b * Y[0]) + dminus * gm;
-              float dgam = dminus * Y[1];
-              if (valid) {
-                dbeta += ca[0] + cb[0] * (b - mu[0]);
-                dgam += ca[1] + cb[1] * (gm - mu[1]);
-              } else {
-                dbeta = 0.f; dgam = 0.f;
-              }
-              rec[go + 2 * r] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
-              rec[go + 2 * r + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
-              dyf[sl][0] = dS; dyf[sl][1] = dI;
+              const float fa = rec[fo + 3 * r + c];
+              float dfa = M::HAS_P ? A.fa_w * dres[c] : dres[c];
+              dfa = valid ? dfa + cn * fa : 0.f;
+              rec[go + 3 * r + c] = dfa;
             }
           }
-        });
+          float dS = 0.f, dI = 0.f;
+          if constexpr (M::HAS_P) {
+            constexpr int qo = M::act_off(0, M::nl(0) - 1);
+            constexpr int go = M::gbuf(0, M::nl(0) - 1);
+            const float q0 = rec[qo + 2 * r], q1 = rec[qo + 2 * r + 1];
+            const float b = fabsf(q0), gm = fabsf(q1);
+            const float dplus = dres[1] - dres[0];
+            const float dminus = dres[2] - dres[1];
+            const float dpi = dplus * Y[1];                 // d(beta*S)
+            float dbeta = dpi * Y[0];
+            dS = dpi * b;
+            dI = dplus * (b * Y[0]) + dminus * gm;
+            float dgam = dminus * Y[1];
+            if (valid) {
+              dbeta += ca[0] + cb[0] * (b - mu[0]);
+              dgam += ca[1] + cb[1] * (gm - mu[1]);
+            } else {
+              dbeta = 0.f; dgam = 0.f;
+            }
+            rec[go + 2 * r] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
+            rec[go + 2 * r + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
+          }
+          rec[M::RK_DYF + 2 * r] = dS;
+          rec[M::RK_DYF + 2 * r + 1] = dI;
+        }
         // zero the padded rows of the final-layer gradient slots
         if constexpr (M::HAS_P) {
           constexpr int lo = 2 * M::R, hi = M::kout(0, M::nl(0) - 1);
+          #pragma unroll 1
           for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
             const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
             lds[t * SR + M::gbuf(0, M::nl(0) - 1) + o] = 0.f;
@@ -582,63 +674,81 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
         if constexpr (M::HAS_A) {
           constexpr int lo = 3 * M::R, hi = M::kout(1, M::nl(1) - 1);
+          #pragma unroll 1
           for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
             const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
             lds[t * SR + M::gbuf(1, M::nl(1) - 1) + o] = 0.f;
           }
         }
+        UDE_STAMP(pf, 6);
         __syncthreads();
-        mlp_backward<M, W, SR>(A.pack, lds, dw, gacc, g0t, lane);
+        UDE_STAMP(pf, 11);
+        mlp_backward<M, W, SR>(rs, lds, dw, g0t, lane, pf);
 
-        // RK4 (3/8 rule) adjoint of the stage combination
-        sfor<SL>([&](auto ss) {
-          constexpr int sl = decltype(ss)::value;
-          const int p = tid + sl * NTHREADS;
-          if (p < M::PAIRS) {
-            const int r = p / TT, t = p - r * TT;
+        // RK4 (3/8 rule) adjoint of the stage inputs
+        //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
+        #pragma unroll 1
+        for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+          const int r = p / TT, t = p - r * TT;
+          float* rec = lds + t * SR;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              float dY = lds[t * SR + M::GY_OFF + 3 * r + c];
-              if (c < 2) dY += dyf[sl][c];
-              accy[sl][c] += dY;
-              if (jj == 3) {
-                const float u = dt * dY;
-                dk1[sl][c] += u; dk2[sl][c] -= u; dk3[sl][c] += u;
-              } else if (jj == 2) {
-                const float u = dt * dY;
-                dk2[sl][c] += u; dk1[sl][c] -= u * (1.0f / 3.0f);
-              } else if (jj == 1) {
-                dk1[sl][c] += (dY * (1.0f / 3.0f)) * dt;
-              }
+          for (int c = 0; c < 3; ++c) {
+            const int f = 3 * r + c;
+            float dY = rec[M::GY_OFF + f];
+            if (c < 2) dY += rec[M::RK_DYF + 2 * r + c];
+            rec[M::RK_ACCY + f] += dY;
+            if (jj == 3) {
+              const float u = dt * dY;
+              rec[M::RK_DK1 + f] += u; rec[M::RK_DK2 + f] -= u; rec[M::RK_DK3 + f] += u;
+            } else if (jj == 2) {
+              const float u = dt * dY;
+              rec[M::RK_DK2 + f] += u; rec[M::RK_DK1 + f] -= u * (1.0f / 3.0f);
+            } else if (jj == 1) {
+              rec[M::RK_DK1 + f] += (dY * (1.0f / 3.0f)) * dt;
             }
           }
-        });
+        }
+        UDE_STAMP(pf, 12);
       }
-#pragma unroll
-      for (int sl = 0; sl < SL; ++sl)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) a[sl][c] = accy[sl][c] + pend[sl][c];
-    }
-
-    // ---- tile end: dy0 (dynamic), static-feature gradients, bias sums ----
-    sfor<SL>([&](auto ss) {
-      constexpr int sl = decltype(ss)::value;
-      const int p = tid + sl * NTHREADS;
-      if (p < M::PAIRS) {
+      #pragma unroll 1
+      for (int p = tid; p < M::PAIRS; p += NTHREADS) {
         const int r = p / TT, t = p - r * TT;
-        const int n = n0 + t;
-        if (n < A.n_traj) {
-          const size_t base = ((size_t)n * M::R + r) * M::L;
+        float* rec = lds + t * SR;
 #pragma unroll
-          for (int c = 0; c < 3; ++c) A.dy0[base + c] = a[sl][c] + A.dlatent[base + c];
+        for (int c = 0; c < 3; ++c) {
+          const int f = 3 * r + c;
+          rec[M::RK_A + f] = rec[M::RK_ACCY + f] + rec[M::RK_PEND + f];
         }
       }
-    });
+    }
+
+    // ---- tile end: dy0 (dynamic), static-feature gradients, layer-0 bias sums ----
+    #pragma unroll 1
+    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+      const int r = p / TT, t = p - r * TT;
+      const int n = n0 + t;
+      if (n < A.n_traj) {
+        const size_t base = ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] + A.dlatent[base + c];
+      }
+    }
     __syncthreads();
     sfor<M::FT(0)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(0, k) == W) {
-        *reinterpret_cast<f4*>(lds + t16 * SR + M::G0_OFF + k * 16 + g * 4) = g0t[M::nz_before(W, k)];
+        const f4 gv = g0t[M::nz_before(W, k)];
+        *reinterpret_cast<f4*>(lds + t16 * SR + M::G0_OFF + k * 16 + g * 4) = gv;
+        f4 r = gv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+        }
+        if (t16 == 0) {
+          float* db = lds + M::DB_LDS + k * 16 + g * 4;
+          db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+        }
       }
     });
     load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
@@ -661,8 +771,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
       });
       // dy0[:, static] = W0[:, static]^T G0 + sum_j dlatent[j][:, static]
-      for (int rt = (tid >> 6); rt < M::NCS; rt += WAVES) {
-        f4 acc = gemm_tile<M::K0>(A.pack + M::WST_OFF + rt * (M::K0 / 16) * 256, lds + t16 * SR + M::G0_OFF, lane, f4zero());
+      sfor<M::NCS>([&](auto rr) {
+        constexpr int rt = decltype(rr)::value;
+        if constexpr (rt % WAVES != W) return;
+        f4 acc = gemm_tile<M::K0, M::WST_OFF + rt * (M::K0 / 16) * 256>(rs, lds + t16 * SR + M::G0_OFF, lane, f4zero());
         const int n = n0 + t16;
         if (n < A.n_traj) {
 #pragma unroll
@@ -672,21 +784,18 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
               const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
               const size_t base = ((size_t)n * M::R + r) * M::L + c;
               float v = acc[e];
+              #pragma unroll 1
               for (int jo = 0; jo <= A.n_out; ++jo) v += A.dlatent[(size_t)jo * NRL + base];
               A.dy0[base] = v;
             }
           }
         }
-      }
+      });
     }
-    sfor<M::FT(0)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(0, k) == W) gacc[M::ng_before(W, 0, k)] += g0t[M::nz_before(W, k)];
-    });
     __syncthreads();
   }
 
-  // ---- kernel end: register tiles -> this workgroup's slab ----
+  // ---- kernel end: register tiles + LDS row sums -> this workgroup's slab ----
   sfor<M::D>([&](auto dd) {
     constexpr int d = decltype(dd)::value;
     sfor<M::FT(d)>([&](auto kk) {
@@ -697,18 +806,14 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           constexpr int ct = decltype(cc)::value;
           reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
         });
-        f4 gv = gacc[M::ng_before(W, d, k)];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = gv[e];
-          v += __shfl_xor(v, 1, 64); v += __shfl_xor(v, 2, 64);
-          v += __shfl_xor(v, 4, 64); v += __shfl_xor(v, 8, 64);
-          gv[e] = v;
-        }
-        if (t16 == 0) *reinterpret_cast<f4*>(myslab + M::SLAB_DB + (M::FTbase(d) + k) * 16 + g * 4) = gv;
       }
     });
   });
+  #pragma unroll 1
+  for (int i = tid; i < 16 * M::FTbase_total(); i += NTHREADS) myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
+#ifdef UDE_PROFILE
+  if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
+#endif
 }
 
 template <class M>

@@ -53,6 +53,7 @@ struct Model {
   // ---- forward row tiles at depth d: P tiles first, then A tiles -------------
   static constexpr int FT(int d) { return rto(0, d) + rto(1, d); }
   static constexpr int FTbase(int d) { int s = 0; for (int e = 0; e < d; ++e) s += FT(e); return s; }
+  static constexpr int FTbase_total() { return FTbase(D); }
   static constexpr int fnet(int d, int k) { return k < rto(0, d) ? 0 : 1; }
   static constexpr int frt(int d, int k) { return k < rto(0, d) ? k : k - rto(0, d); }
   static constexpr int fowner(int d, int k) { return (FTbase(d) + k) % WAVES; }
@@ -95,15 +96,26 @@ struct Model {
   }
   static constexpr int gbuf(int net, int i) { return gb_off(net, i & 1); }
   static constexpr int GY_OFF = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);
+  // backward-only RK4 adjoint state, one [t][F] vector each (see bwd_body)
+  static constexpr int F4 = (F + 3) & ~3;
+  static constexpr int RK_A = GY_OFF + F16;       // adjoint of y_{n+1} (carried across steps)
+  static constexpr int RK_PEND = RK_A + F4;       // y_n-side share of interpolated outputs
+  static constexpr int RK_ACCY = RK_PEND + F4;    // adjoint of y_n being accumulated
+  static constexpr int RK_DK1 = RK_ACCY + F4;
+  static constexpr int RK_DK2 = RK_DK1 + F4;
+  static constexpr int RK_DK3 = RK_DK2 + F4;
+  static constexpr int RK_DYF = RK_DK3 + F4;      // direct d flux / d (S, I) of the current stage ([t][2R])
   static constexpr int REC_F = cmax(ACT_END, F16 + S16);
-  static constexpr int REC_B = GY_OFF + F16;
+  static constexpr int REC_B = RK_DYF + ((2 * R + 3) & ~3);
   // row stride == 4 (mod 64) floats: conflict-free b128 fragment reads, and rows
   // t and t+4 land 16 banks apart for the dW b32 reads.
   static constexpr int stride(int n) { return ((n + 59) / 64) * 64 + 4; }
   static constexpr int SR_F = stride(REC_F);
   static constexpr int SR_B = stride(REC_B);
   static constexpr int LDS_F = TT * SR_F * 4;
-  static constexpr int LDS_B = TT * SR_B * 4;
+  // + per-workgroup bias-gradient row sums (one float per forward row tile row)
+  static constexpr int DB_LDS = TT * SR_B;
+  static constexpr int LDS_B = (TT * SR_B + 16 * FTbase_total()) * 4;
 
   // ---- packed weights (fragment order, 16-B per lane per MFMA quad) --------------
   //  WF(net,i): [rto][kin/16][64 lanes][4]   A operand of the forward GEMM

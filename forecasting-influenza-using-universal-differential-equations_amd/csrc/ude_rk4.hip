@@ -20,6 +20,10 @@ const ude::Entry* find(const UdeModelDesc* m) {
 }
 }  // namespace
 
+#ifdef UDE_PROFILE
+namespace ude { unsigned long long* g_prof_buffer = nullptr; }
+#endif
+
 extern "C" {
 
 int ude_supported(const UdeModelDesc* m) { return find(m) ? 1 : 0; }
@@ -57,6 +61,10 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
   return e->backward(p, pack, sched, y0, ckpt, dlatent, stats_out, dstats, dy0, grad_slab, dparams,
                      (hipStream_t)stream);
 }
+
+#ifdef UDE_PROFILE
+void ude_debug_set_prof(unsigned long long* p) { ude::g_prof_buffer = p; }
+#endif
 
 const char* ude_build_info(void) {
   return "ude_rk4 gfx950: v_mfma_f32_16x16x4_f32, TT=16, 4 waves/WG, registry=" UDE_REGISTRY_TAG;

@@ -142,7 +142,8 @@ def _run(cmd: List[str]) -> None:
         raise UdeError("build command failed:\n" + " ".join(cmd) + "\n" + r.stdout[-8000:])
 
 
-def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: Optional[int] = None) -> str:
+def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: Optional[int] = None,
+                  extra_flags: Sequence[str] = ()) -> str:
     """Compile one object per configuration + the C-ABI, link into out_path."""
     if not os.path.exists(HIPCC):
         raise UdeError(f"hipcc not found ({HIPCC}); cannot build the gfx950 library")
@@ -156,7 +157,7 @@ def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: O
     reg.append(f'#define UDE_REGISTRY_TAG "{tag}:{len(cfgs)}"')
     with open(os.path.join(gen, "ude_registry.inc"), "w") as f:
         f.write("\n".join(reg) + "\n")
-    inc = ["-I", INCLUDE, "-I", CSRC, "-I", gen]
+    inc = ["-I", INCLUDE, "-I", CSRC, "-I", gen, *extra_flags]
 
     def compile_cfg(i_cfg):
         i, cfg = i_cfg

@@ -1,0 +1,56 @@
+"""Diagnostic: per-segment cycle breakdown of the backward kernel's stage loop.
+
+Builds a -DUDE_PROFILE copy of one configuration (s_memtime stamps at every
+barrier of the stage loop, thread 0 of each workgroup), runs the bench workload
+through it and prints the average cycles per stage spent in each segment.  The
+stamped build is slower than the real one; read the shares, not the totals.
+"""
+import ctypes
+import importlib
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+pkg = importlib.import_module("forecasting-influenza-using-universal-differential-equations_amd")
+from ude_amd import _native  # noqa: E402
+import bench  # noqa: E402
+
+SEG = {0: "ckpt load (+outputs)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1", 4: "fwd d2", 5: "fwd d3",
+       6: "flux bwd", 11: "barrier after flux", 10: "bwd d3", 9: "bwd d2", 8: "bwd d1", 7: "bwd d0",
+       12: "RK adjoint"}
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "state49"
+    w = bench.WORKLOADS[wl]
+    cfg = (w["kind"], w["R"], w["L"], tuple(w["net"]) if w["net"] else None, tuple(w["aug"]) if w["aug"] else None)
+    path = os.path.join(_native.BUILD, "libude_rk4_profile.so")
+    _native.build_library([cfg], path, "profile", jobs=1, extra_flags=["-DUDE_PROFILE"])
+    lib = _native.NativeLib(path)
+    lib.lib.ude_debug_set_prof.argtypes = [ctypes.c_void_p]
+    _native.library_for = lambda c: lib
+    dev = torch.device("cuda", 0)
+    mod, y0, t, dlat = bench.build(pkg, w, dev, seed=1)
+    from ude_amd import distributed as udist
+    bench.one_step(pkg, udist, mod, y0, t, dlat, 1)        # warm up (grid size known after)
+    buf = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+    lib.lib.ude_debug_set_prof(buf.data_ptr())
+    bench.one_step(pkg, udist, mod, y0, t, dlat, 1)
+    torch.cuda.synchronize()
+    lib.lib.ude_debug_set_prof(None)
+    v = buf.view(-1, 16).double()
+    used = v[v.sum(1) > 0]
+    tiles = (w["n_traj"] + 15) // 16
+    stages = tiles * 4 * (len(t) - 1) / used.shape[0]
+    per = used.mean(0) / stages
+    tot = float(per.sum())
+    print(f"workgroups {used.shape[0]}, stages per WG {stages:.1f}, cycles per stage {tot:.0f}")
+    for k in sorted(SEG, key=lambda s: [0, 1, 2, 3, 4, 5, 6, 11, 10, 9, 8, 7, 12].index(s)):
+        print(f"  {SEG[k]:24s} {float(per[k]):9.0f}  {100 * float(per[k]) / tot:5.1f}%")
+
+
+if __name__ == "__main__":
+    main()

@@ -185,20 +185,24 @@ def main():
     ap.add_argument("--workload", default="state49", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch.distributed as dist
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
         barrier = lambda: dist.barrier()
     else:
         barrier = lambda: None
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
 
     pkg = importlib.import_module(PKG)
     from ude_amd import distributed as udist

@@ -41,7 +41,7 @@ def _worker(rank, port, q):
         gf = fa.grad.clone()
         # gradient averaging across ranks as in all_reduce_grads: grads here are per-rank
         # contributions d(sum_r loss_r)/d p_local, which must equal WORLD x the single-process grad
-        q.put((rank, float(n_tot), m.detach(), s.detach(), nrm.detach(), gp, gf, lo, hi))
+        q.put((rank, float(n_tot), m.detach().numpy(), s.detach().numpy(), nrm.detach().numpy(), gp.numpy(), gf.numpy(), lo, hi))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -67,6 +67,7 @@ def test_combine_stats_matches_single_process():
         + (s * torch.tensor([0.5, 0.1], dtype=torch.float64)).sum() + 0.1 * nrm
     loss.backward()
     for rank, n_tot, rm, rs, rn, gp, gf, lo, hi in res:
+        rm, rs, rn, gp, gf = (torch.from_numpy(x) for x in (rm, rs, rn, gp, gf))
         assert n_tot == 300
         assert torch.allclose(rm, m.detach()) and torch.allclose(rs, s.detach())
         assert torch.allclose(rn, nrm.detach().reshape(1))

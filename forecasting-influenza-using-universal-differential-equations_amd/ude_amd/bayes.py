@@ -1,0 +1,155 @@
+"""Bayesian UDE right-hand sides (lib/in_development/models_bayes.py:12-265).
+
+Every Linear is a ``Dense_Variational``: on EACH call a fresh weight sample
+``w = mu + eps * |sigma|`` (:43-48), so every RHS evaluation inside a solve
+sees new weights.  Same names, constructor signatures, ``state_dict`` keys
+(``w_mean``, ``w_std``, ``b_mean``, ``b_std``) and ``get_kl`` as the reference.
+
+These run eagerly (PyTorch ops per evaluation): the fused kernel needs the
+per-evaluation noise streams injected, which is the next row of the build plan
+(SURVEY section 8f, rank 1).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+import torch.distributions as dist
+
+from .rhs import _UDEModule, _finish, _run_stack, _sir_flux
+
+
+class Dense_Variational(nn.Module):
+    def __init__(self, in_features, out_features, bias=True, prior_std=1.0):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.prior_std = prior_std
+        self.w_mean = nn.Parameter(torch.empty(out_features, in_features))
+        self.w_std = nn.Parameter(torch.empty(out_features, in_features))
+        if bias:
+            self.bias = True
+            self.b_mean = nn.Parameter(torch.empty(out_features))
+            self.b_std = nn.Parameter(torch.empty(out_features))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.kaiming_uniform_(self.w_mean, a=math.sqrt(5))
+        nn.init.constant_(self.w_std, 0.1)
+        if self.bias is not None:
+            bound = 1.0 / math.sqrt(self.in_features)
+            nn.init.uniform_(self.b_mean, -bound, bound)
+            nn.init.constant_(self.b_std, 0.1)
+
+    def make_z(self):
+        with torch.no_grad():
+            self.z = [torch.randn_like(self.w_mean), torch.randn_like(self.b_mean)]
+
+    def forward(self, x):
+        self.make_z()
+        w = self.w_mean + self.z[0] * torch.abs(self.w_std)
+        b = self.b_mean + self.z[1] * torch.abs(self.b_std)
+        return nn.functional.linear(x, w, b)
+
+    def make_prior(self):
+        s = self.prior_std
+        self.prior = [dist.Normal(torch.zeros_like(self.w_mean), s * torch.ones_like(self.w_mean)),
+                      dist.Normal(torch.zeros_like(self.b_mean), s * torch.ones_like(self.b_mean))]
+        return self.prior
+
+    def make_posterior(self):
+        self.posterior = [dist.Normal(self.w_mean, torch.abs(self.w_std)),
+                          dist.Normal(self.b_mean, torch.abs(self.b_std))]
+        return self.posterior
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
+
+
+def _variational_stack(n_in, sizes, n_out, prior_std, lead_flatten=True):
+    mods = [nn.Flatten()] if lead_flatten else []
+    widths = [n_in] + list(sizes)
+    mods.append(Dense_Variational(widths[0], widths[1], prior_std=prior_std))
+    for a, b in zip(widths[1:-1], widths[2:]):
+        mods.extend([nn.ELU(inplace=True), Dense_Variational(a, b, prior_std=prior_std)])
+    mods.append(Dense_Variational(widths[-1], n_out, prior_std=prior_std))
+    return nn.ModuleList(mods)
+
+
+def _kl_of(stacks):
+    total, count = 0, 0
+    for stack in stacks:
+        for layer in stack:
+            if isinstance(layer, Dense_Variational):
+                kls = [dist.kl_divergence(q, p).mean() for q, p in zip(layer.make_posterior(), layer.make_prior())]
+                total = total + sum(kls) / 2
+                count += 1
+    return total / count
+
+
+class _BayesBase(_UDEModule):
+    uncertainty = "bayes"
+
+
+class Bayes_Fp(_BayesBase):
+    def __init__(self, n_regions=1, latent_dim=8, net_sizes=[20, 20], prior_std=0.1, **kwargs):
+        super().__init__()
+        self.n_regions, self.latent_dim = n_regions, latent_dim
+        self.ode_type, self.uncertainty = "Fp", "bayes"
+        self._p_sizes = list(net_sizes)
+        self.Fp_net = _variational_stack(n_regions * latent_dim, net_sizes, 2 * n_regions, prior_std)
+        self._init_tracking()
+
+    def forward(self, t, x):
+        rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
+        self.params.append(rates)
+        return _finish(_sir_flux(rates, x), x)
+
+    def get_kl(self):
+        return _kl_of([self.Fp_net])
+
+
+class Bayes_Fa(_BayesBase):
+    def __init__(self, n_regions=1, latent_dim=8, aug_net_sizes=[32, 32], nhidden_fa=32, prior_std=0.1, **kwargs):
+        super().__init__()
+        self.n_regions, self.latent_dim = n_regions, latent_dim
+        self.ode_type, self.uncertainty = "Fa", "bayes"
+        self._a_sizes = list(aug_net_sizes)
+        self.aug_net = _variational_stack(n_regions * latent_dim, aug_net_sizes, 3 * n_regions, prior_std)
+        self._init_tracking()
+
+    def forward(self, t, x):
+        fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
+        res = _finish(fa, x)
+        self.tracker.append(fa)
+        return res
+
+    def get_kl(self):
+        return _kl_of([self.aug_net])
+
+
+class Bayes_FaFp(_BayesBase):
+    def __init__(self, n_regions=1, latent_dim=8, net_sizes=[20, 20], aug_net_sizes=[32, 32], prior_std=0.1,
+                 **kwargs):
+        super().__init__()
+        self.n_regions, self.latent_dim = n_regions, latent_dim
+        self.ode_type, self.uncertainty = "FaFp", "bayes"
+        self._p_sizes, self._a_sizes = list(net_sizes), list(aug_net_sizes)
+        self.Fp_net = _variational_stack(n_regions * latent_dim, net_sizes, 2 * n_regions, prior_std)
+        self.aug_net = _variational_stack(n_regions * latent_dim, aug_net_sizes, 3 * n_regions, prior_std)
+        self.Fa_w = 1.0
+        self._init_tracking()
+
+    def forward(self, t, x):
+        rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
+        self.params.append(rates)
+        fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
+        res = _finish(_sir_flux(rates, x) + self.Fa_w * fa, x)
+        self.tracker.append(fa)
+        return res
+
+    def get_kl(self):
+        return _kl_of([self.Fp_net, self.aug_net])

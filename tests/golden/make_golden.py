@@ -176,5 +176,65 @@ def main():
     print("rhs fixtures written")
 
 
+
+
+def make_e2e():
+    """End-to-end training-step fixture: the reference VAE (lib/VAE.py) with the
+    reference Encoder / Decoder / FaFp, integrated by the oracle RK4 (injected as
+    the `torchdiffeq` module the reference imports), one train-step loss + grads."""
+    import types
+    import torch.nn as nn
+    td = types.ModuleType("torchdiffeq")
+
+    def _odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None):
+        assert method == "rk4"
+        return odeint_rk4(func, y0, t, (options or {}).get("step_size"))
+    td.odeint = _odeint
+    sys.modules["torchdiffeq"] = td
+    import lib.VAE as ref_vae
+    torch.manual_seed(4242)
+    B, window, n_qs, S_ = 4, 6, 3, 5
+    model = ref_vae.VAE(ref_models.Encoder_Back_GRU, ref_models.FaFp, ref_models.Decoder, n_qs, 8, 1,
+                        ode_params={"net_sizes": [16, 16, 8], "aug_net_sizes": [16, 12], "prior_std": 0.05},
+                        enc_params={"q_sizes": [16, 8], "ff_sizes": [8, 8], "SIR_scaler": [0.1, 0.05, 1.0]},
+                        uncertainty=True, ode_kl_w=1 / 153)
+    model.setup_training(lr=1e-3)
+    gen = torch.Generator().manual_seed(99)
+    x = torch.rand(B, window, n_qs + 1, generator=gen)
+    gamma = 21
+    t = torch.arange(window + gamma + 1, dtype=torch.float32) / 7
+    eval_pts = np.arange(0, 22, 7)                      # run_ode.py curriculum stage [0, 7, 14, 21]
+    y = torch.rand(B, len(t), 1, generator=gen) * 0.5
+    y[0, 3, 0] = -1.0                                   # masked target (train_functions.nll_loss)
+    losses = {"nll": True, "mse": False, "kl_z": True, "kl_p": True, "Fa_norm": 1e-1, "reg_loss": True, "anneal": True}
+    sd = {"enc": {k: v.clone() for k, v in model.enc.state_dict().items()},
+          "ode": {k: v.clone() for k, v in model.ode.state_dict().items()},
+          "dec": {k: v.clone() for k, v in model.dec.state_dict().items()}}
+    torch.manual_seed(7)
+    eps = torch.randn(S_, B, 1, model.ld_enc)
+    torch.manual_seed(7)                                # VAE.__call__ draws the same eps
+    model.optimizer.zero_grad()
+    y_pred = model(x, t[eval_pts], n_samples=S_, training=True)
+    loss, data, names = model.calc_loss(y_pred, y[:, eval_pts, :], losses)
+    loss.backward()
+    arrs = {"x": x.numpy(), "y": y.numpy(), "t": t.numpy(), "eval_pts": eval_pts, "eps": eps.numpy(),
+            "loss": np.array([float(loss)]), "y_pred": y_pred.detach().numpy(),
+            "latent": model.latent.detach().numpy()}
+    for part, mod in (("enc", model.enc), ("ode", model.ode), ("dec", model.dec)):
+        for k, v in sd[part].items():
+            arrs[f"w_{part}.{k}"] = v.numpy()
+        for k, p in mod.named_parameters():
+            arrs[f"g_{part}.{k}"] = p.grad.detach().numpy()
+    meta = {"B": B, "window": window, "n_qs": n_qs, "n_samples": S_, "losses": losses,
+            "loss_names": names, "loss_data": data,
+            "ode_params": {"net_sizes": [16, 16, 8], "aug_net_sizes": [16, 12]},
+            "enc_params": {"q_sizes": [16, 8], "ff_sizes": [8, 8], "SIR_scaler": [0.1, 0.05, 1.0]}}
+    arrs["meta_json"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(HERE, "e2e_vae_step.npz"), **arrs)
+    print("e2e fixture written, loss", float(loss), dict(zip(names, data)))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 1:
+        main()
+    make_e2e()

@@ -58,6 +58,12 @@ struct Ops {
     return UDE_OK;
   }
 
+  // grad-slab workspace tail: G0 [tile][K0][16] + split-K partials [chunks][K0][S16]
+  static int64_t static_ws_floats(int n_tiles) {
+    if (M::S == 0) return 0;
+    return (int64_t)n_tiles * M::K0 * TT + (int64_t)M::STATIC_CHUNKS * M::K0 * M::S16;
+  }
+
   static int query(const UdeProblem* p, int device, UdeSizes* o) {
     if (p->n_traj < 1 || p->n_steps < 0 || p->n_out < 0) return UDE_E_INVALID;
     const int n_tiles = (p->n_traj + TT - 1) / TT;
@@ -68,7 +74,7 @@ struct Ops {
     o->sched_bytes = (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
     o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * M::F * TT * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
-    o->grad_slab_bytes = (int64_t)gb * M::SLAB_TOTAL * 4;
+    o->grad_slab_bytes = (int64_t)gb * M::SLAB_TOTAL * 4 + static_ws_floats(n_tiles) * 4;
     o->n_params = M::N_PARAMS;
     o->grid_fwd = gf;
     o->grid_bwd = gb;
@@ -87,7 +93,7 @@ struct Ops {
         P.W[net][i] = W[li];
         P.b[net][i] = b[li];
       }
-    int mx = M::WST_SIZE;
+    int mx = M::W0SP_SIZE;
     for (int net = 0; net < 2; ++net) {
       if (M::wsf_size(net) > mx) mx = M::wsf_size(net);
       for (int i = 0; i < M::nl(net); ++i) {
@@ -142,6 +148,9 @@ struct Ops {
     a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
     a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.stats_out = stats_out; a.dstats = dstats;
     a.dy0 = dy0; a.slab = slab;
+    float* g0buf = slab + (size_t)gb * M::SLAB_TOTAL;
+    float* part = g0buf + (size_t)n_tiles * M::K0 * TT;
+    a.g0buf = g0buf;
 #ifdef UDE_PROFILE
     a.prof = g_prof_buffer;
 #endif
@@ -152,6 +161,18 @@ struct Ops {
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::N_PARAMS + 255) / 256), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());
+    if (M::S > 0) {
+      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::K0 / 16, M::S16 / 16, M::STATIC_CHUNKS), dim3(256), 0, s,
+                         (const float*)g0buf, y0, p->n_traj, n_tiles, part);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
+                         (const float*)part, dparams);
+      HIPCHK(hipGetLastError());
+      const size_t nel = (size_t)p->n_traj * M::S;
+      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, s,
+                         (const float*)g0buf, pack, dlatent, p->n_traj, p->n_out + 1, dy0);
+      HIPCHK(hipGetLastError());
+    }
     return UDE_OK;
   }
 };

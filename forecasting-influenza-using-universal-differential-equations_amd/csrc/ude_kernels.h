@@ -62,6 +62,7 @@ struct KArgs {
   int n_traj, n_steps, n_out, n_tiles;
   float fa_w;
   unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
+  float* g0buf;               // backward: per-trajectory layer-0 gradient sums [tile][K0][16]
 };
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
@@ -121,14 +122,19 @@ __device__ __forceinline__ f4 gemm_tile(Rsrc rs, const float* bp, int lane, f4 a
   constexpr int KQ = KP / 4;
   constexpr int NQ = KP / 16;
   const float* b = bp + (lane >> 4) * KQ;
+  // every A fragment of the tile is issued before the first MFMA (the scheduler
+  // otherwise serialises load -> wait -> 4 MFMAs, paying the L2 latency per quad)
+  f4 a[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) a[q] = ldw(rs, lane * 16, (WOFF + q * 256) * 4);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const f4 a = ldw(rs, lane * 16, (WOFF + q * 256) * 4);
     const f4 x = *reinterpret_cast<const f4*>(b + 4 * q);
-    acc = mfma4(a[0], x[0], acc);
-    acc = mfma4(a[1], x[1], acc);
-    acc = mfma4(a[2], x[2], acc);
-    acc = mfma4(a[3], x[3], acc);
+    acc = mfma4(a[q][0], x[0], acc);
+    acc = mfma4(a[q][1], x[1], acc);
+    acc = mfma4(a[q][2], x[2], acc);
+    acc = mfma4(a[q][3], x[3], acc);
   }
   return acc;
 }
@@ -515,8 +521,6 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 #endif
 
   #pragma unroll 1
-  for (int i = tid; i < M::SLAB_DB - M::SLAB_STATIC; i += NTHREADS) myslab[M::SLAB_STATIC + i] = 0.f;
-  #pragma unroll 1
   for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;
   __syncthreads();
 
@@ -734,11 +738,16 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       }
     }
     __syncthreads();
+    // per-trajectory layer-0 gradient sums -> global (static-feature gradients are
+    // computed from them by ude_static_*_kernel); their trajectory sums -> bias row sums
     sfor<M::FT(0)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(0, k) == W) {
         const f4 gv = g0t[M::nz_before(W, k)];
-        *reinterpret_cast<f4*>(lds + t16 * SR + M::G0_OFF + k * 16 + g * 4) = gv;
+        if constexpr (M::S > 0) {
+          float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
+          dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
+        }
         f4 r = gv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -751,47 +760,6 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
       }
     });
-    load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
-    __syncthreads();
-    if constexpr (M::S > 0) {
-      // dW0[:, static] += sum_t G0[t][o] * x_static[t][s]   (read-modify-write of this WG's slab)
-      sfor<M::FT(0)>([&](auto kk) {
-        constexpr int k = decltype(kk)::value;
-        if constexpr (M::fowner(0, k) == W) {
-          float ga[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + M::G0_OFF + k * 16 + t16];
-          for (int cs = 0; cs < M::NCS; ++cs) {
-            f4* dst = reinterpret_cast<f4*>(myslab + M::SLAB_STATIC + (k * M::NCS + cs) * 256) + lane;
-            f4 acc = *dst;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) acc = mfma4(ga[s], lds[(4 * g + s) * SR + M::XSB_OFF + cs * 16 + t16], acc);
-            *dst = acc;
-          }
-        }
-      });
-      // dy0[:, static] = W0[:, static]^T G0 + sum_j dlatent[j][:, static]
-      sfor<M::NCS>([&](auto rr) {
-        constexpr int rt = decltype(rr)::value;
-        if constexpr (rt % WAVES != W) return;
-        f4 acc = gemm_tile<M::K0, M::WST_OFF + rt * (M::K0 / 16) * 256>(rs, lds + t16 * SR + M::G0_OFF, lane, f4zero());
-        const int n = n0 + t16;
-        if (n < A.n_traj) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int s = rt * 16 + g * 4 + e;
-            if (s < M::S) {
-              const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
-              const size_t base = ((size_t)n * M::R + r) * M::L + c;
-              float v = acc[e];
-              #pragma unroll 1
-              for (int jo = 0; jo <= A.n_out; ++jo) v += A.dlatent[(size_t)jo * NRL + base];
-              A.dy0[base] = v;
-            }
-          }
-        }
-      });
-    }
     __syncthreads();
   }
 
@@ -885,11 +853,10 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
     }
   });
   if constexpr (M::S > 0) {
-    if (seg == 32 && idx < M::WST_SIZE) {
-      constexpr int KQ = M::K0 / 4, NQ = M::K0 / 16;
-      const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
-      int om = (ln >> 4) * KQ + 4 * q + e;
-      const int s = rt * 16 + (ln & 15);
+    if (seg == 32 && idx < M::W0SP_SIZE) {
+      // plain [merged layer-0 row][static feature] copy (dy0 static kernel)
+      int om = idx / M::S16;
+      const int s = idx - om * M::S16;
       int net = 0;
       if (!M::HAS_P || om >= (M::HAS_P ? M::kout(0, 0) : 0)) {
         net = 1;
@@ -899,7 +866,7 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
       float v = 0.f;
       if (s < M::S && om < out && (net == 0 ? M::HAS_P : M::HAS_A))
         v = P.W[net][0][(size_t)om * M::R * M::L + static_col<M>(s)];
-      pack[M::WST_OFF + idx] = v;
+      pack[M::W0SP_OFF + idx] = v;
     }
   }
 }
@@ -935,7 +902,7 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
           }
           const int lane = (row >> 2) * 16 + (f & 15), reg = row & 3;
           if (!stat) off = (M::dyn_tiles_before(i, k) + f / 16) * 256 + lane * 4 + reg;
-          else off = M::SLAB_STATIC + (k * M::NCS + f / 16) * 256 + lane * 4 + reg;
+          else off = -2;   // static column: written by ude_static_reduce_kernel
         } else if (e >= b0 && e < b0 + out) {
           const int o = e - b0;
           off = M::SLAB_DB + (M::FTbase(i) + kbase + o / 16) * 16 + (o % 16);
@@ -943,9 +910,84 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
       }
     });
   });
+  if (off < 0) return;
   float s = 0.f;
   for (int gi = 0; gi < ngrid; ++gi) s += slab[(size_t)gi * M::SLAB_TOTAL + off];
   dparams[e] = s;
+}
+
+// ============================================================================
+// Static-feature gradients (latent dims >= 3 are per-trajectory constants):
+//   dW0[o][static s] = sum_n G0[n][o] * y0[n][static s]
+//   dy0[n][static s] = sum_o W0[o][static s] * G0[n][o] + sum_j dlatent[j][n][static s]
+// with G0[n][o] = sum over every evaluation of the layer-0 output gradient.
+// ============================================================================
+template <class M>
+__global__ __launch_bounds__(256) void ude_static_partial_kernel(const float* __restrict__ g0buf,
+                                                                 const float* __restrict__ y0, int n_traj,
+                                                                 int n_tiles, float* __restrict__ part) {
+  __shared__ float sg[TT][16 + 1], sx[TT][16 + 1];
+  const int ot = blockIdx.x, st = blockIdx.y, chunk = blockIdx.z;
+  const int tid = threadIdx.x, oo = tid >> 4, ss = tid & 15;
+  const int per = (n_tiles + M::STATIC_CHUNKS - 1) / M::STATIC_CHUNKS;
+  const int t_beg = chunk * per, t_end = min(n_tiles, t_beg + per);
+  float acc = 0.f;
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    // G0 tile [16 rows][16 trajectories] and the matching static inputs [16 traj][16 feats]
+    sg[ss][oo] = g0buf[((size_t)tile * M::K0 + ot * 16 + oo) * TT + ss];
+    const int n = tile * TT + oo, sfeat = st * 16 + ss;
+    float xv = 0.f;
+    if (n < n_traj && sfeat < M::S) {
+      const int r = sfeat / (M::L - 3), c = 3 + sfeat - r * (M::L - 3);
+      xv = y0[((size_t)n * M::R + r) * M::L + c];
+    }
+    sx[oo][ss] = xv;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TT; ++t) acc += sg[t][oo] * sx[t][ss];
+    __syncthreads();
+  }
+  part[((size_t)chunk * M::K0 + ot * 16 + oo) * M::S16 + st * 16 + ss] = acc;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void ude_static_reduce_kernel(const float* __restrict__ part,
+                                                                float* __restrict__ dparams) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= M::K0 * M::S) return;
+  const int om = e / M::S, s = e - om * M::S;
+  int net = 0, o = om;
+  if (!M::HAS_P || om >= (M::HAS_P ? M::kout(0, 0) : 0)) {
+    net = 1;
+    o = om - (M::HAS_P ? M::kout(0, 0) : 0);
+  }
+  const int out = net == 0 ? M::out_dim(0, 0) : M::out_dim(1, 0);
+  if (o >= out) return;
+  float v = 0.f;
+  for (int c = 0; c < M::STATIC_CHUNKS; ++c) v += part[((size_t)c * M::K0 + om) * M::S16 + s];
+  const int w0 = net == 0 ? M::param_w_off(0, 0) : M::param_w_off(1, 0);
+  dparams[w0 + (size_t)o * M::R * M::L + static_col<M>(s)] = v;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __restrict__ g0buf,
+                                                             const float* __restrict__ pack,
+                                                             const float* __restrict__ dlatent, int n_traj,
+                                                             int n_times, float* __restrict__ dy0) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (size_t)n_traj * M::S) return;
+  const int n = (int)(idx / M::S), s = (int)(idx - (size_t)n * M::S);
+  const int tile = n / TT, tt = n - tile * TT;
+  const float* g = g0buf + (size_t)tile * M::K0 * TT + tt;
+  const float* w = pack + M::W0SP_OFF + s;
+  float v = 0.f;
+#pragma unroll 8
+  for (int o = 0; o < M::K0; ++o) v += w[o * M::S16] * g[o * TT];
+  const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
+  const size_t base = ((size_t)n * M::R + r) * M::L + c;
+  const size_t NRL = (size_t)n_traj * M::R * M::L;
+  for (int j = 0; j < n_times; ++j) v += dlatent[(size_t)j * NRL + base];
+  dy0[base] = v;
 }
 
 template <int V_ = 0>

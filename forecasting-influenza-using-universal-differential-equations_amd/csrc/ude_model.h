@@ -122,7 +122,7 @@ struct Model {
   //  WT(net,i): [rti][kout/16][64][4]        A operand of the input-gradient GEMM
   //  B(net,i):  [kout]                       bias, zero padded
   //  WSF(net):  [rto(net,0)][S16/16][64][4]  layer-0 static columns (per-tile hoist)
-  //  WST:       [S16/16][K0/16][64][4]       layer-0 static columns, transposed, merged nets
+  //  W0SP:      [K0][S16]                    layer-0 static columns, plain, merged nets (dy0 static)
   static constexpr int wf_size(int net, int i) { return has(net, i) ? rto(net, i) * (kin(net, i) / 16) * 256 : 0; }
   static constexpr int wt_size(int net, int i) { return has(net, i) ? rti(net, i) * (kout(net, i) / 16) * 256 : 0; }
   static constexpr int b_size(int net, int i) { return has(net, i) ? kout(net, i) : 0; }
@@ -142,9 +142,9 @@ struct Model {
   static constexpr int LAYERS_END = layer_pack_off(2, 0);
   static constexpr int wsf_size(int net) { return (S > 0 && has(net, 0)) ? rto(net, 0) * (S16 / 16) * 256 : 0; }
   static constexpr int wsf_off(int net) { return LAYERS_END + (net == 0 ? 0 : wsf_size(0)); }
-  static constexpr int WST_OFF = LAYERS_END + wsf_size(0) + wsf_size(1);
-  static constexpr int WST_SIZE = S > 0 ? (S16 / 16) * (K0 / 16) * 256 : 0;
-  static constexpr int PACK_TOTAL = WST_OFF + WST_SIZE;
+  static constexpr int W0SP_OFF = LAYERS_END + wsf_size(0) + wsf_size(1);
+  static constexpr int W0SP_SIZE = S > 0 ? K0 * S16 : 0;
+  static constexpr int PACK_TOTAL = W0SP_OFF + W0SP_SIZE;
 
   // ---- per-workgroup gradient slab -------------------------------------------------
   static constexpr int dyn_tiles_before(int d, int k) {
@@ -158,9 +158,11 @@ struct Model {
   }
   static constexpr int N_DYN_TILES = dyn_tiles_before(D, 0);
   static constexpr int NCS = S16 / 16;
-  static constexpr int SLAB_STATIC = N_DYN_TILES * 256;
-  static constexpr int SLAB_DB = SLAB_STATIC + FT(0) * NCS * 256;
+  static constexpr int SLAB_DB = N_DYN_TILES * 256;
   static constexpr int SLAB_TOTAL = SLAB_DB + FTbase(D) * 16;
+  // static-feature gradient work (outside the main kernel): per-tile layer-0 row sums
+  // G0[tile][K0][16] and split-K partials of dW0[:, static]
+  static constexpr int STATIC_CHUNKS = 16;
 
   // ---- per-wave register tiles -----------------------------------------------------
   static constexpr int ndw_before(int w, int d, int k) {

@@ -139,6 +139,28 @@ __device__ __forceinline__ f4 gemm_tile(Rsrc rs, const float* bp, int lane, f4 a
   return acc;
 }
 
+// Split form: issue a tile's fragments into a caller array (so several tiles, or a
+// whole phase, can be in flight before the first MFMA), then run the MFMA chain.
+template <int KP, int WOFF>
+__device__ __forceinline__ void load_frags(Rsrc rs, int lane, f4* fr) {
+#pragma unroll
+  for (int q = 0; q < KP / 16; ++q) fr[q] = ldw(rs, lane * 16, (WOFF + q * 256) * 4);
+}
+template <int KP>
+__device__ __forceinline__ f4 mma_frags(const f4* fr, const float* bp, int lane, f4 acc) {
+  constexpr int KQ = KP / 4;
+  const float* b = bp + (lane >> 4) * KQ;
+#pragma unroll
+  for (int q = 0; q < KP / 16; ++q) {
+    const f4 x = *reinterpret_cast<const f4*>(b + 4 * q);
+    acc = mfma4(fr[q][0], x[0], acc);
+    acc = mfma4(fr[q][1], x[1], acc);
+    acc = mfma4(fr[q][2], x[2], acc);
+    acc = mfma4(fr[q][3], x[3], acc);
+  }
+  return acc;
+}
+
 __device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : expm1f(x); }
 
 template <class M, int NZ_>
@@ -153,6 +175,19 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto dd) {
     constexpr int d = decltype(dd)::value;
+    constexpr int NF = M::FQ(W, d);
+    // all of this wave's weight fragments (and biases) for the phase are in flight
+    // before its first MFMA
+    f4 fr[NF > 0 ? NF : 1], bias[M::FT(d) > 0 ? M::FT(d) : 1];
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
+        load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
+        if constexpr (!(d == 0 && M::S > 0)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
@@ -161,18 +196,14 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
         constexpr int KP = M::kin(net, d);
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
         f4 acc;
-        if constexpr (d == 0 && M::S > 0) {
-          acc = c1[M::nz_before(W, k)];
-        } else {
-          acc = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
-        }
-        acc = gemm_tile<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, rec + inoff, lane, acc);
+        if constexpr (d == 0 && M::S > 0) acc = c1[M::nz_before(W, k)];
+        else acc = bias[k];
+        acc = mma_frags<KP>(fr + M::fq_before(W, d, k), rec + inoff, lane, acc);
         if constexpr (M::act(net, d)) {
           acc[0] = elu1(acc[0]); acc[1] = elu1(acc[1]);
           acc[2] = elu1(acc[2]); acc[3] = elu1(acc[3]);
         }
         *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = acc;
-        __builtin_amdgcn_sched_barrier(0);   // bound live ranges: one tile's fragments at a time
       }
     });
     __syncthreads();
@@ -404,6 +435,26 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
     constexpr int d = M::D - 1 - decltype(ee)::value;
+    // input-gradient fragments go out first; the LDS-only dW GEMMs below hide them
+    constexpr int NX = M::XQ(W, d);
+    f4 fx[NX > 0 ? NX : 1];
+    sfor<M::XT(d)>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      if constexpr (M::xowner(d, m) == W) {
+        constexpr int q0 = M::xq_before(W, d, m);
+        if constexpr (d == 0) {
+          if constexpr (M::HAS_P)
+            load_frags<M::kout(0, 0), M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256>(rs, lane, fx + q0);
+          if constexpr (M::HAS_A)
+            load_frags<M::kout(1, 0), M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256>(
+                rs, lane, fx + q0 + (M::HAS_P ? M::kout(0, 0) / 16 : 0));
+        } else {
+          constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
+          load_frags<M::kout(net, d), M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256>(rs, lane, fx + q0);
+        }
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
     // (1) rows owned by this wave: bias/G sums and the dW GEMM (K = trajectories)
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -448,19 +499,17 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
         if constexpr (d == 0) {
+          constexpr int q0 = M::xq_before(W, d, m);
           f4 acc = f4zero();
-          if constexpr (M::HAS_P)
-            acc = gemm_tile<M::kout(0, 0), M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256>(
-                rs, rec + M::gbuf(0, 0), lane, acc);
+          if constexpr (M::HAS_P) acc = mma_frags<M::kout(0, 0)>(fx + q0, rec + M::gbuf(0, 0), lane, acc);
           if constexpr (M::HAS_A)
-            acc = gemm_tile<M::kout(1, 0), M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256>(
-                rs, rec + M::gbuf(1, 0), lane, acc);
+            acc = mma_frags<M::kout(1, 0)>(fx + q0 + (M::HAS_P ? M::kout(0, 0) / 16 : 0), rec + M::gbuf(1, 0),
+                                           lane, acc);
           *reinterpret_cast<f4*>(rec + M::GY_OFF + m * 16 + g * 4) = acc;
         } else {
           constexpr int net = M::xnet(d, m);
           constexpr int rt = M::xrt(d, m);
-          f4 acc = gemm_tile<M::kout(net, d), M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256>(
-              rs, rec + M::gbuf(net, d), lane, f4zero());
+          f4 acc = mma_frags<M::kout(net, d)>(fx + M::xq_before(W, d, m), rec + M::gbuf(net, d), lane, f4zero());
           if constexpr (M::act(net, d - 1)) {
             const f4 av = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
 #pragma unroll
@@ -617,8 +666,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         mlp_forward<M, W, SR>(rs, lds, c1, lane, pf);
 
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y
-        #pragma unroll 1
-        for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          if (p >= M::PAIRS) return;
           const int r = p / TT, t = p - r * TT;
           const bool valid = n0 + t < A.n_traj;
           float* rec = lds + t * SR;
@@ -666,7 +717,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           }
           rec[M::RK_DYF + 2 * r] = dS;
           rec[M::RK_DYF + 2 * r + 1] = dI;
-        }
+        });
         // zero the padded rows of the final-layer gradient slots
         if constexpr (M::HAS_P) {
           constexpr int lo = 2 * M::R, hi = M::kout(0, M::nl(0) - 1);
@@ -691,8 +742,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 
         // RK4 (3/8 rule) adjoint of the stage inputs
         //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
-        #pragma unroll 1
-        for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+        sfor<SL>([&](auto ss) {
+          constexpr int sl = decltype(ss)::value;
+          const int p = tid + sl * NTHREADS;
+          if (p >= M::PAIRS) return;
           const int r = p / TT, t = p - r * TT;
           float* rec = lds + t * SR;
 #pragma unroll
@@ -711,7 +764,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
               rec[M::RK_DK1 + f] += (dY * (1.0f / 3.0f)) * dt;
             }
           }
-        }
+        });
         UDE_STAMP(pf, 12);
       }
       #pragma unroll 1

@@ -192,6 +192,23 @@ struct Model {
   }
   static constexpr int NZ(int w) { return nz_before(w, FT(0)); }
 
+  // weight-fragment quads (16-B per lane) a wave prefetches per phase
+  static constexpr int fq_before(int w, int d, int k) {
+    int s = 0;
+    for (int kk = 0; kk < k; ++kk) if (fowner(d, kk) == w) s += kin(fnet(d, kk), d) / 16;
+    return s;
+  }
+  static constexpr int FQ(int w, int d) { return fq_before(w, d, FT(d)); }
+  static constexpr int xq(int d, int m) {
+    return d == 0 ? (HAS_P ? kout(0, 0) / 16 : 0) + (HAS_A ? kout(1, 0) / 16 : 0) : kout(xnet(d, m), d) / 16;
+  }
+  static constexpr int xq_before(int w, int d, int m) {
+    int s = 0;
+    for (int mm = 0; mm < m; ++mm) if (xowner(d, mm) == w) s += xq(d, mm);
+    return s;
+  }
+  static constexpr int XQ(int w, int d) { return xq_before(w, d, XT(d)); }
+
   // ---- parameters in torch order (nn.Linear weight (out,in) then bias) ----------------
   static constexpr int param_w_off(int net, int i) {
     int o = 0;

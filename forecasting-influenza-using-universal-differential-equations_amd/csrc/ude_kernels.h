@@ -161,7 +161,12 @@ __device__ __forceinline__ f4 mma_frags(const f4* fr, const float* bp, int lane,
   return acc;
 }
 
-__device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : expm1f(x); }
+// ELU (alpha 1).  expm1 is evaluated unconditionally on min(x, 0) and selected,
+// so the compiler emits straight-line code instead of a divergent branch per value.
+__device__ __forceinline__ float elu1(float x) {
+  const float e = expm1f(fminf(x, 0.f));
+  return x > 0.f ? x : e;
+}
 
 template <class M, int NZ_>
 using C1Arr = f4[NZ_ > 0 ? NZ_ : 1];
@@ -188,22 +193,54 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
       }
     });
     __builtin_amdgcn_sched_barrier(0);
+    f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
-        constexpr int net = M::fnet(d, k);
-        constexpr int rt = M::frt(d, k);
+        if constexpr (d == 0 && M::S > 0) acc[k] = c1[M::nz_before(W, k)];
+        else acc[k] = bias[k];
+      }
+    });
+    // the wave's tiles of one net share the B operand (the layer input): one LDS
+    // read feeds every tile, and consecutive MFMAs go to different accumulators
+    sfor<2>([&](auto nn) {
+      constexpr int net = decltype(nn)::value;
+      if constexpr (M::owns_f(W, d, net)) {
         constexpr int KP = M::kin(net, d);
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
-        f4 acc;
-        if constexpr (d == 0 && M::S > 0) acc = c1[M::nz_before(W, k)];
-        else acc = bias[k];
-        acc = mma_frags<KP>(fr + M::fq_before(W, d, k), rec + inoff, lane, acc);
-        if constexpr (M::act(net, d)) {
-          acc[0] = elu1(acc[0]); acc[1] = elu1(acc[1]);
-          acc[2] = elu1(acc[2]); acc[3] = elu1(acc[3]);
+        const float* b = rec + inoff + g * (KP / 4);
+        // B quads are read in chunks of QB ahead of their MFMAs (one LDS wait per chunk)
+        constexpr int NQ = KP / 16, QB = 5;
+#pragma unroll
+        for (int q0 = 0; q0 < NQ; q0 += QB) {
+          f4 xb[QB];
+#pragma unroll
+          for (int q = q0; q < q0 + QB && q < NQ; ++q) xb[q - q0] = *reinterpret_cast<const f4*>(b + 4 * q);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = q0; q < q0 + QB && q < NQ; ++q) {
+            const f4 x = xb[q - q0];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              sfor<M::FT(d)>([&](auto kk) {
+                constexpr int k = decltype(kk)::value;
+                if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net)
+                  acc[k] = mfma4(fr[M::fq_before(W, d, k) + q][e], x[e], acc[k]);
+              });
+          }
         }
-        *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = acc;
+      }
+    });
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k), rt = M::frt(d, k);
+        f4 a = acc[k];
+        if constexpr (M::act(net, d)) {
+          a[0] = elu1(a[0]); a[1] = elu1(a[1]);
+          a[2] = elu1(a[2]); a[3] = elu1(a[3]);
+        }
+        *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = a;
       }
     });
     __syncthreads();
@@ -417,7 +454,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 }
 
 template <class M, bool TRAIN>
-__global__ __launch_bounds__(NTHREADS) void ude_fwd_kernel(KArgs a) {
+__global__ __launch_bounds__(NTHREADS, 2) void ude_fwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w == 0) fwd_body<M, TRAIN, 0>(a, lds);
@@ -429,8 +466,36 @@ __global__ __launch_bounds__(NTHREADS) void ude_fwd_kernel(KArgs a) {
 // ============================================================================
 // Backward (VJP)
 // ============================================================================
-template <class M, int W, int SR, class DW, class G0>
-__device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0t, int lane, Prof* pf = nullptr) {
+// RK4 (3/8 rule) adjoint of the stage input, MLP part: consumes the layer-0 input
+// gradient dY (4 features x 1 trajectory per lane) straight from the dX tile's
+// registers (see the flux section of bwd_body for the direct part).
+template <class M, int SR>
+struct RkAdjointEp {
+  float* rec;      // this lane's trajectory record
+  float dt;
+  int jj;          // RK stage (3..0)
+  __device__ __forceinline__ void operator()(int f0, f4 dY) const {
+    if (f0 >= M::F4) return;                       // padded feature rows
+    f4* accy = reinterpret_cast<f4*>(rec + M::RK_ACCY + f0);
+    f4* dk1 = reinterpret_cast<f4*>(rec + M::RK_DK1 + f0);
+    f4* dk2 = reinterpret_cast<f4*>(rec + M::RK_DK2 + f0);
+    f4* dk3 = reinterpret_cast<f4*>(rec + M::RK_DK3 + f0);
+    *accy += dY;
+    if (jj == 3) {
+      const f4 u = dt * dY;
+      *dk1 += u; *dk2 -= u; *dk3 += u;
+    } else if (jj == 2) {
+      const f4 u = dt * dY;
+      *dk2 += u; *dk1 -= u * (1.0f / 3.0f);
+    } else if (jj == 1) {
+      *dk1 += (dY * (1.0f / 3.0f)) * dt;
+    }
+  }
+};
+
+template <class M, int W, int SR, class DW, class G0, class EP0>
+__device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0t, int lane, Prof* pf,
+                                             const EP0& ep0) {
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
@@ -480,36 +545,68 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
             db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
           }
         }
-        float ga[4];
+        // all of the tile's LDS operands are read before its first MFMA: one LDS
+        // latency per tile instead of one per MFMA pair
+        constexpr int NC = M::rti(net, d);
+        float ga[4], bv[4][NC];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
-        sfor<M::rti(net, d)>([&](auto cc) {
-          constexpr int ct = decltype(cc)::value;
-          constexpr int idx = M::ndw_before(W, d, k) + ct;
-          f4 acc = dw[idx];
+        for (int s = 0; s < 4; ++s) {
+          ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma4(ga[s], lds[(4 * g + s) * SR + inoff + ct * 16 + t], acc);
-          dw[idx] = acc;
-        });
+          for (int ct = 0; ct < NC; ++ct) bv[s][ct] = lds[(4 * g + s) * SR + inoff + ct * 16 + t];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // s outer: consecutive MFMAs update different dW tiles (no accumulator chain)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          sfor<NC>([&](auto cc) {
+            constexpr int ct = decltype(cc)::value;
+            constexpr int idx = M::ndw_before(W, d, k) + ct;
+            dw[idx] = mfma4(ga[s], bv[s][ct], dw[idx]);
+          });
         __builtin_amdgcn_sched_barrier(0);
       }
     });
-    // (2) gradient w.r.t. the layer input (rows = input features)
+    // (2) gradient w.r.t. the layer input (rows = input features); tiles sharing a
+    // B operand (the same net's output gradient) are interleaved
+    f4 xa[M::XT(d) > 0 ? M::XT(d) : 1];
+    sfor<M::XT(d)>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      if constexpr (M::xowner(d, m) == W) xa[m] = f4zero();
+    });
+    sfor<2>([&](auto nn) {
+      constexpr int net = decltype(nn)::value;
+      if constexpr (M::has(net, d) && M::owns_x(W, d, net)) {
+        constexpr int KP = M::kout(net, d);
+        // d == 0: both nets' fragments of a tile sit back to back (P first)
+        constexpr int qoff = (d == 0 && net == 1 && M::HAS_P) ? M::kout(0, 0) / 16 : 0;
+        const float* b = rec + M::gbuf(net, d) + g * (KP / 4);
+        f4 xb[KP / 16];
+#pragma unroll
+        for (int q = 0; q < KP / 16; ++q) xb[q] = *reinterpret_cast<const f4*>(b + 4 * q);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < KP / 16; ++q) {
+          const f4 x = xb[q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sfor<M::XT(d)>([&](auto mm) {
+              constexpr int m = decltype(mm)::value;
+              if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net))
+                xa[m] = mfma4(fx[M::xq_before(W, d, m) + qoff + q][e], x[e], xa[m]);
+            });
+        }
+      }
+    });
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
+        f4 acc = xa[m];
         if constexpr (d == 0) {
-          constexpr int q0 = M::xq_before(W, d, m);
-          f4 acc = f4zero();
-          if constexpr (M::HAS_P) acc = mma_frags<M::kout(0, 0)>(fx + q0, rec + M::gbuf(0, 0), lane, acc);
-          if constexpr (M::HAS_A)
-            acc = mma_frags<M::kout(1, 0)>(fx + q0 + (M::HAS_P ? M::kout(0, 0) / 16 : 0), rec + M::gbuf(1, 0),
-                                           lane, acc);
-          *reinterpret_cast<f4*>(rec + M::GY_OFF + m * 16 + g * 4) = acc;
+          ep0(m * 16 + g * 4, acc);
         } else {
           constexpr int net = M::xnet(d, m);
           constexpr int rt = M::xrt(d, m);
-          f4 acc = mma_frags<M::kout(net, d)>(fx + M::xq_before(W, d, m), rec + M::gbuf(net, d), lane, f4zero());
           if constexpr (M::act(net, d - 1)) {
             const f4 av = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
 #pragma unroll
@@ -517,12 +614,130 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
           }
           *reinterpret_cast<f4*>(rec + M::gbuf(net, d - 1) + rt * 16 + g * 4) = acc;
         }
-        __builtin_amdgcn_sched_barrier(0);
       }
     });
     __syncthreads();
     UDE_STAMP(pf, 7 + d);
   });
+}
+
+// Flux backward for one RK stage (reference RHS, lib/models.py:130-150):
+//   dS = -beta S I, dI = beta S I - gamma I, dR = gamma I  (+ fa_w * Fa for FaFp),
+// masked where a state leaves (-1, 2); beta = |q0|, gamma = |q1|.  Writes the
+// final-layer gradients (d q, d Fa incl. the |Fa| and posterior side-statistic
+// terms) and applies the direct (d flux / d S, I) part of the RK adjoint.
+template <class M, int SR>
+__device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0, int jj, float dt,
+                                              const float* ca, const float* cb, const float* mu, float cn) {
+  constexpr int RG = (M::R + 3) / 4, ITEMS = TT * RG;
+  constexpr int QO = M::HAS_P ? M::act_off(0, M::nl(0) - 1) : 0, QG = M::HAS_P ? M::gbuf(0, M::nl(0) - 1) : 0;
+  constexpr int FO = M::HAS_A ? M::act_off(1, M::nl(1) - 1) : 0, FG = M::HAS_A ? M::gbuf(1, M::nl(1) - 1) : 0;
+  constexpr bool VEC_Q = !M::HAS_P || M::QW <= M::kout(0, M::nl(0) - 1);
+  constexpr bool VEC_F = !M::HAS_A || M::F4 <= M::kout(1, M::nl(1) - 1);
+  #pragma unroll 1
+  for (int it = threadIdx.x; it < ITEMS; it += NTHREADS) {
+    const int t = it & (TT - 1), rg = it >> 4;
+    const bool valid = n0 + t < A.n_traj;
+    float* rec = lds + t * SR;
+    float Y[12], dk[12], dres[12];
+    const int f0 = 12 * rg;
+    const int dko = jj == 3 ? M::RK_A : jj == 2 ? M::RK_DK3 : jj == 1 ? M::RK_DK2 : M::RK_DK1;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const f4 y = *reinterpret_cast<const f4*>(rec + M::Y_OFF + f0 + 4 * v);
+      const f4 k = *reinterpret_cast<const f4*>(rec + dko + f0 + 4 * v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { Y[4 * v + e] = y[e]; dk[4 * v + e] = k[e]; }
+    }
+    if (jj == 3) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) dk[i] = (dk[i] * 0.125f) * dt;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const bool live = valid && (4 * rg + i / 3) < M::R;
+      dres[i] = (!live || Y[i] > 2.f || Y[i] < -1.f) ? 0.f : dk[i];
+    }
+    if constexpr (M::HAS_A) {
+      float dfa[12];
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const f4 fa = *reinterpret_cast<const f4*>(rec + FO + f0 + 4 * v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * v + e;
+          const bool live = valid && (4 * rg + i / 3) < M::R;
+          const float d = M::HAS_P ? A.fa_w * dres[i] : dres[i];
+          dfa[i] = live ? d + cn * fa[e] : 0.f;
+        }
+      }
+      if constexpr (VEC_F) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          f4 o = {dfa[4 * v], dfa[4 * v + 1], dfa[4 * v + 2], dfa[4 * v + 3]};
+          *reinterpret_cast<f4*>(rec + FG + f0 + 4 * v) = o;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+          if (f0 + i < M::kout(1, M::nl(1) - 1)) rec[FG + f0 + i] = dfa[i];
+      }
+    }
+    float dyf[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) dyf[i] = 0.f;
+    if constexpr (M::HAS_P) {
+      float q[8], dq[8];
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const f4 x = *reinterpret_cast<const f4*>(rec + QO + 8 * rg + 4 * v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[4 * v + e] = x[e];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool live = valid && (4 * rg + j) < M::R;
+        const float* y = Y + 3 * j;
+        const float* dr = dres + 3 * j;
+        const float q0 = q[2 * j], q1 = q[2 * j + 1];
+        const float b = fabsf(q0), gm = fabsf(q1);
+        const float dplus = dr[1] - dr[0];
+        const float dminus = dr[2] - dr[1];
+        const float dpi = dplus * y[1];                 // d(beta*S)
+        float dbeta = dpi * y[0];
+        dyf[3 * j] = dpi * b;
+        dyf[3 * j + 1] = dplus * (b * y[0]) + dminus * gm;
+        float dgam = dminus * y[1];
+        if (live) {
+          dbeta += ca[0] + cb[0] * (b - mu[0]);
+          dgam += ca[1] + cb[1] * (gm - mu[1]);
+        } else {
+          dbeta = 0.f; dgam = 0.f;
+        }
+        dq[2 * j] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
+        dq[2 * j + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
+      }
+      if constexpr (VEC_Q) {
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          f4 o = {dq[4 * v], dq[4 * v + 1], dq[4 * v + 2], dq[4 * v + 3]};
+          *reinterpret_cast<f4*>(rec + QG + 8 * rg + 4 * v) = o;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (8 * rg + i < M::kout(0, M::nl(0) - 1)) rec[QG + 8 * rg + i] = dq[i];
+      }
+      // RK4 (3/8 rule) adjoint of the stage input, direct (flux) part; the MLP part
+      // is added by mlp_backward's layer-0 epilogue (RkAdjointEp)
+      //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const f4 dY = {dyf[4 * v], dyf[4 * v + 1], dyf[4 * v + 2], dyf[4 * v + 3]};
+        RkAdjointEp<M, SR>{rec, dt, jj}(f0 + 4 * v, dY);
+      }
+    }
+  }
 }
 
 template <class M, int W>
@@ -665,62 +880,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 1);
         mlp_forward<M, W, SR>(rs, lds, c1, lane, pf);
 
-        // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y
-        sfor<SL>([&](auto ss) {
-          constexpr int sl = decltype(ss)::value;
-          const int p = tid + sl * NTHREADS;
-          if (p >= M::PAIRS) return;
-          const int r = p / TT, t = p - r * TT;
-          const bool valid = n0 + t < A.n_traj;
-          float* rec = lds + t * SR;
-          float Y[3], dres[3];
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int f = 3 * r + c;
-            Y[c] = rec[M::Y_OFF + f];
-            const float dk = jj == 3 ? (rec[M::RK_A + f] * 0.125f) * dt
-                           : rec[(jj == 2 ? M::RK_DK3 : jj == 1 ? M::RK_DK2 : M::RK_DK1) + f];
-            dres[c] = (!valid || Y[c] > 2.f || Y[c] < -1.f) ? 0.f : dk;
-          }
-          if constexpr (M::HAS_A) {
-            constexpr int fo = M::act_off(1, M::nl(1) - 1);
-            constexpr int go = M::gbuf(1, M::nl(1) - 1);
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const float fa = rec[fo + 3 * r + c];
-              float dfa = M::HAS_P ? A.fa_w * dres[c] : dres[c];
-              dfa = valid ? dfa + cn * fa : 0.f;
-              rec[go + 3 * r + c] = dfa;
-            }
-          }
-          float dS = 0.f, dI = 0.f;
-          if constexpr (M::HAS_P) {
-            constexpr int qo = M::act_off(0, M::nl(0) - 1);
-            constexpr int go = M::gbuf(0, M::nl(0) - 1);
-            const float q0 = rec[qo + 2 * r], q1 = rec[qo + 2 * r + 1];
-            const float b = fabsf(q0), gm = fabsf(q1);
-            const float dplus = dres[1] - dres[0];
-            const float dminus = dres[2] - dres[1];
-            const float dpi = dplus * Y[1];                 // d(beta*S)
-            float dbeta = dpi * Y[0];
-            dS = dpi * b;
-            dI = dplus * (b * Y[0]) + dminus * gm;
-            float dgam = dminus * Y[1];
-            if (valid) {
-              dbeta += ca[0] + cb[0] * (b - mu[0]);
-              dgam += ca[1] + cb[1] * (gm - mu[1]);
-            } else {
-              dbeta = 0.f; dgam = 0.f;
-            }
-            rec[go + 2 * r] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
-            rec[go + 2 * r + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
-          }
-          rec[M::RK_DYF + 2 * r] = dS;
-          rec[M::RK_DYF + 2 * r + 1] = dI;
-        });
+        // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
+        // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
+        // every record access is a 16-B LDS op.
+        flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         // zero the padded rows of the final-layer gradient slots
         if constexpr (M::HAS_P) {
-          constexpr int lo = 2 * M::R, hi = M::kout(0, M::nl(0) - 1);
+          constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
           #pragma unroll 1
           for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
             const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
@@ -728,7 +894,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           }
         }
         if constexpr (M::HAS_A) {
-          constexpr int lo = 3 * M::R, hi = M::kout(1, M::nl(1) - 1);
+          constexpr int lo = cmin(M::F4, M::kout(1, M::nl(1) - 1)), hi = M::kout(1, M::nl(1) - 1);
           #pragma unroll 1
           for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
             const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
@@ -738,33 +904,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);
-        mlp_backward<M, W, SR>(rs, lds, dw, g0t, lane, pf);
+        mlp_backward<M, W, SR>(rs, lds, dw, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj});
 
-        // RK4 (3/8 rule) adjoint of the stage inputs
-        //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
-        sfor<SL>([&](auto ss) {
-          constexpr int sl = decltype(ss)::value;
-          const int p = tid + sl * NTHREADS;
-          if (p >= M::PAIRS) return;
-          const int r = p / TT, t = p - r * TT;
-          float* rec = lds + t * SR;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const int f = 3 * r + c;
-            float dY = rec[M::GY_OFF + f];
-            if (c < 2) dY += rec[M::RK_DYF + 2 * r + c];
-            rec[M::RK_ACCY + f] += dY;
-            if (jj == 3) {
-              const float u = dt * dY;
-              rec[M::RK_DK1 + f] += u; rec[M::RK_DK2 + f] -= u; rec[M::RK_DK3 + f] += u;
-            } else if (jj == 2) {
-              const float u = dt * dY;
-              rec[M::RK_DK2 + f] += u; rec[M::RK_DK1 + f] -= u * (1.0f / 3.0f);
-            } else if (jj == 1) {
-              rec[M::RK_DK1 + f] += (dY * (1.0f / 3.0f)) * dt;
-            }
-          }
-        });
         UDE_STAMP(pf, 12);
       }
       #pragma unroll 1

@@ -18,6 +18,7 @@ constexpr int NTHREADS = WAVES * 64;
 
 constexpr int pad16(int x) { return (x + 15) & ~15; }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
 enum : int { KIND_FP = 1, KIND_FA = 2, KIND_FAFP = 3 };
 
@@ -95,18 +96,19 @@ struct Model {
     return ALIAS_END + (net == 0 ? 0 : 2 * gbs(0)) + parity * gbs(net);
   }
   static constexpr int gbuf(int net, int i) { return gb_off(net, i & 1); }
-  static constexpr int GY_OFF = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);
   // backward-only RK4 adjoint state, one [t][F] vector each (see bwd_body)
-  static constexpr int F4 = (F + 3) & ~3;
-  static constexpr int RK_A = GY_OFF + F16;       // adjoint of y_{n+1} (carried across steps)
+  // RK-state vectors are 12 * ceil(R/4) wide: the flux backward works on groups of
+  // 4 regions (12 features) with 16-B LDS ops; QW = the matching width of the rates
+  static constexpr int F4 = 12 * ((R + 3) / 4);
+  static constexpr int QW = 8 * ((R + 3) / 4);
+  static constexpr int RK_A = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);  // adjoint of y_{n+1} (carried across steps)
   static constexpr int RK_PEND = RK_A + F4;       // y_n-side share of interpolated outputs
   static constexpr int RK_ACCY = RK_PEND + F4;    // adjoint of y_n being accumulated
   static constexpr int RK_DK1 = RK_ACCY + F4;
   static constexpr int RK_DK2 = RK_DK1 + F4;
   static constexpr int RK_DK3 = RK_DK2 + F4;
-  static constexpr int RK_DYF = RK_DK3 + F4;      // direct d flux / d (S, I) of the current stage ([t][2R])
   static constexpr int REC_F = cmax(ACT_END, F16 + S16);
-  static constexpr int REC_B = RK_DYF + ((2 * R + 3) & ~3);
+  static constexpr int REC_B = RK_DK3 + F4;
   // row stride == 4 (mod 64) floats: conflict-free b128 fragment reads, and rows
   // t and t+4 land 16 banks apart for the dW b32 reads.
   static constexpr int stride(int n) { return ((n + 59) / 64) * 64 + 4; }
@@ -199,6 +201,14 @@ struct Model {
     return s;
   }
   static constexpr int FQ(int w, int d) { return fq_before(w, d, FT(d)); }
+  static constexpr bool owns_f(int w, int d, int net) {
+    for (int k = 0; k < FT(d); ++k) if (fowner(d, k) == w && fnet(d, k) == net) return true;
+    return false;
+  }
+  static constexpr bool owns_x(int w, int d, int net) {
+    for (int m = 0; m < XT(d); ++m) if (xowner(d, m) == w && (d == 0 || xnet(d, m) == net)) return true;
+    return false;
+  }
   static constexpr int xq(int d, int m) {
     return d == 0 ? (HAS_P ? kout(0, 0) / 16 : 0) + (HAS_A ? kout(1, 0) / 16 : 0) : kout(xnet(d, m), d) / 16;
   }

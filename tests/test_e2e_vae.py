@@ -60,7 +60,7 @@ def _check(g, model, loss, y_pred, names, tol):
 def test_vae_step_cpu_matches_reference(pkg, monkeypatch):
     g = load_golden("e2e_vae_step")
     model, loss, y_pred, names, data = _step(pkg, g, "cpu", monkeypatch)
-    _check(g, model, loss, y_pred, names, 1e-6)
+    _check(g, model, loss, y_pred, names, 1e-5)  # fp32 CPU reductions differ across host ISAs (AVX2 vs AVX-512)
 
 
 @pytest.mark.gpu

@@ -127,7 +127,7 @@ struct Ops {
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
     HIPCHK(hipGetLastError());
     return UDE_OK;
   }
@@ -158,18 +158,17 @@ struct Ops {
     a.fa_w = p->fa_w;
     hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::N_PARAMS + 255) / 256), dim3(256), 0, s,
+    hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());
     if (M::S > 0) {
-      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::K0 / 16, M::S16 / 16, M::STATIC_CHUNKS), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS), dim3(256), 0, s,
                          (const float*)g0buf, y0, p->n_traj, n_tiles, part);
       HIPCHK(hipGetLastError());
       hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
                          (const float*)part, dparams);
       HIPCHK(hipGetLastError());
-      const size_t nel = (size_t)p->n_traj * M::S;
-      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3(n_tiles), dim3(256), 0, s,
                          (const float*)g0buf, pack, dlatent, p->n_traj, p->n_out + 1, dy0);
       HIPCHK(hipGetLastError());
     }

@@ -621,6 +621,61 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
   });
 }
 
+// Cotangents of the outputs written after RK step `step` (torchdiffeq's
+// _linear_interp between y_step and y_step+1): sg = the y_{step+1}-side share,
+// pg = the y_step-side share, per pair slot (p = tid + sl * NTHREADS) and S/I/R.
+template <class M>
+__device__ __forceinline__ void out_shares(const KArgs& A, const Sched& sc, int step, int n0,
+                                           float (&sg)[M::SLOTS][3], float (&pg)[M::SLOTS][3]) {
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+#pragma unroll
+  for (int sl = 0; sl < M::SLOTS; ++sl)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { sg[sl][c] = 0.f; pg[sl][c] = 0.f; }
+  const int o_beg = sc.out_start[step], o_end = sc.out_start[step + 1];
+  #pragma unroll 1
+  for (int o = o_beg; o < o_end; ++o) {
+    const int mode = sc.out_mode[o];
+    const float slope = sc.out_slope[o];
+    const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL;
+    float gv[M::SLOTS][3];
+    sfor<M::SLOTS>([&](auto ss) {
+      constexpr int sl = decltype(ss)::value;
+      const int p = threadIdx.x + sl * NTHREADS;
+      const int r = p / TT, t = p - r * TT, n = n0 + t;
+      const bool valid = p < M::PAIRS && n < A.n_traj;
+      const size_t base = valid ? ((size_t)n * M::R + r) * M::L : 0;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) gv[sl][c] = valid ? gl[base + c] : 0.f;
+    });
+#pragma unroll
+    for (int sl = 0; sl < M::SLOTS; ++sl)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float a = mode == 2 ? slope * gv[sl][c] : (mode == 1 ? gv[sl][c] : 0.f);
+        const float b = mode == 2 ? gv[sl][c] - a : (mode == 0 ? gv[sl][c] : 0.f);
+        sg[sl][c] += a;
+        pg[sl][c] += b;
+      }
+  }
+}
+
+// Issue the loads of one checkpointed stage input ([f][t] per tile-stage in HBM)
+// into registers, slot sl of thread tid holding pair p = tid + sl * NTHREADS.
+template <class M>
+__device__ __forceinline__ void ckpt_issue(const KArgs& A, int tile, int step, int jj, float (&ck)[M::SLOTS][3]) {
+  const Rsrc rck = make_rsrc(A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0), M::F * TT * 4);
+  sfor<M::SLOTS>([&](auto ss) {
+    constexpr int sl = decltype(ss)::value;
+    const int p = threadIdx.x + sl * NTHREADS;
+    const int r = p / TT, t = p - r * TT;
+    const int v = (p < M::PAIRS) ? (3 * r * TT + t) * 4 : 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      ck[sl][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rck, v, c * TT * 4, 0));
+  });
+}
+
 // Flux backward for one RK stage (reference RHS, lib/models.py:130-150):
 //   dS = -beta S I, dI = beta S I - gamma I, dR = gamma I  (+ fa_w * Fa for FaFp),
 // masked where a state leaves (-1, 2); beta = |q0|, gamma = |q1|.  Writes the
@@ -796,75 +851,71 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       const int t = i / M::F;
       lds[t * SR + M::RK_A + (i - t * M::F)] = 0.f;
     }
-    __syncthreads();
-    static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
-#pragma unroll
-    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
-    __syncthreads();
-
-    for (int step = A.n_steps - 1; step >= 0; --step) {
-      const float dt = sc.dt[step];
-      const int o_beg = sc.out_start[step], o_end = sc.out_start[step + 1];
-      // d latent of the outputs written after this step -> adjoint of y_{n+1} / y_n;
-      // then the stage cotangents of the 3/8 combination dy = (k1+3(k2+k3)+k4)*dt/8.
-      // (slots unrolled: every cotangent load of the step is in flight at once)
+    // output cotangents of the last step: y_{n+1} share -> RK_A, y_n share staged in
+    // DK3 (picked up by the step start).  Later steps get theirs under the flux pass
+    // of the previous step's last stage.
+    if (A.n_steps > 0) {
+      float sg[SL][3], pg[SL][3];
+      out_shares<M>(A, sc, A.n_steps - 1, n0, sg, pg);
       sfor<SL>([&](auto ss) {
         constexpr int sl = decltype(ss)::value;
         const int p = tid + sl * NTHREADS;
         if (p < M::PAIRS) {
           const int r = p / TT, t = p - r * TT;
-          const int n = n0 + t;
-          float* rec = lds + t * SR;
-          float a[3], pend[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-          for (int c = 0; c < 3; ++c) a[c] = rec[M::RK_A + 3 * r + c];
-          if (n < A.n_traj) {
-            #pragma unroll 1
-            for (int o = o_beg; o < o_end; ++o) {
-              const int mode = sc.out_mode[o];
-              const float slope = sc.out_slope[o];
-              const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL + ((size_t)n * M::R + r) * M::L;
-#pragma unroll
-              for (int c = 0; c < 3; ++c) {
-                // y1-side / y0-side shares (torchdiffeq _linear_interp)
-                const float gv = gl[c];
-                const float sg = mode == 2 ? slope * gv : (mode == 1 ? gv : 0.f);
-                const float pg = mode == 2 ? gv - sg : (mode == 0 ? gv : 0.f);
-                a[c] += sg;
-                pend[c] += pg;
-              }
-            }
-          }
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            const int f = 3 * r + c;
-            const float sdk = (a[c] * 0.125f) * dt;
-            rec[M::RK_A + f] = a[c];
-            rec[M::RK_PEND + f] = pend[c];
-            rec[M::RK_ACCY + f] = a[c];
-            rec[M::RK_DK1 + f] = sdk;
-            rec[M::RK_DK2 + f] = 3.0f * sdk;
-            rec[M::RK_DK3 + f] = 3.0f * sdk;
+            lds[t * SR + M::RK_A + 3 * r + c] = sg[sl][c];
+            lds[t * SR + M::RK_DK3 + 3 * r + c] = pg[sl][c];
           }
         }
       });
+    }
+    __syncthreads();
+    static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    __syncthreads();
+    UDE_STAMP(pf, 15);
+
+    bool have_next = false;
+    for (int step = A.n_steps - 1; step >= 0; --step) {
+      const float dt = sc.dt[step];
+      // step start: RK_A already holds the adjoint of y_{n+1} including this step's
+      // output cotangents (y_n-side share staged in DK3); set up the accumulators and
+      // the stage cotangents of the 3/8 combination dy = (k1 + 3 (k2 + k3) + k4) dt / 8.
+      {
+        constexpr int NV = M::F4 / 4;
+        #pragma unroll 1
+        for (int i = tid; i < TT * NV; i += NTHREADS) {
+          const int t = i / NV, v = i - t * NV;
+          float* rec = lds + t * SR + 4 * v;
+          const f4 a = *reinterpret_cast<const f4*>(rec + M::RK_A);
+          const f4 pend = *reinterpret_cast<const f4*>(rec + M::RK_DK3);
+          const f4 sdk = (a * 0.125f) * dt;
+          *reinterpret_cast<f4*>(rec + M::RK_PEND) = pend;
+          *reinterpret_cast<f4*>(rec + M::RK_ACCY) = a;
+          *reinterpret_cast<f4*>(rec + M::RK_DK1) = sdk;
+          *reinterpret_cast<f4*>(rec + M::RK_DK2) = 3.0f * sdk;
+          *reinterpret_cast<f4*>(rec + M::RK_DK3) = 3.0f * sdk;
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
+      UDE_STAMP(pf, 14);
 
       for (int jj = 3; jj >= 0; --jj) {
-        // stage input from the forward's checkpoint (one SGPR descriptor per stage,
-        // all slots' loads issued before the first LDS store)
-        {
-          const Rsrc rck = make_rsrc(A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0), M::F * TT * 4);
+        // stage input: from the staging slot the previous stage's flux pass filled,
+        // or (first stage of the tile) straight from the forward's checkpoint
+        if (have_next) {
+          constexpr int NV = TT * (M::F4 / 4);
+          #pragma unroll 1
+          for (int i = tid; i < NV; i += NTHREADS) {
+            const int t = i / (M::F4 / 4), v = i - t * (M::F4 / 4);
+            *reinterpret_cast<f4*>(lds + t * SR + M::Y_OFF + 4 * v) =
+                *reinterpret_cast<const f4*>(lds + M::STG_LDS + t * M::F4 + 4 * v);
+          }
+        } else {
           float ck[SL][3];
-          sfor<SL>([&](auto ss) {
-            constexpr int sl = decltype(ss)::value;
-            const int p = tid + sl * NTHREADS;
-            const int r = p / TT, t = p - r * TT;
-            const int v = (p < M::PAIRS) ? (3 * r * TT + t) * 4 : 0;
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-              ck[sl][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rck, v, c * TT * 4, 0));
-          });
+          ckpt_issue<M>(A, tile, step, jj, ck);
           sfor<SL>([&](auto ss) {
             constexpr int sl = decltype(ss)::value;
             const int p = tid + sl * NTHREADS;
@@ -883,7 +934,42 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
+        // the next stage's checkpointed input is fetched under the flux pass and the
+        // MLP backward (registers only live across the flux pass)
+        const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
+        have_next = nstep >= 0;
+        float ckn[SL][3], sgn[SL][3], pgn[SL][3];
+        if (have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        const bool next_out = jj == 0 && have_next;
+        if (next_out) out_shares<M>(A, sc, nstep, n0, sgn, pgn);
         flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        if (next_out) {
+          // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
+          // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
+          sfor<SL>([&](auto ss) {
+            constexpr int sl = decltype(ss)::value;
+            const int p = tid + sl * NTHREADS;
+            if (p < M::PAIRS) {
+              const int r = p / TT, t = p - r * TT;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) {
+                lds[t * SR + M::RK_PEND + 3 * r + c] += sgn[sl][c];
+                lds[t * SR + M::RK_DK3 + 3 * r + c] = pgn[sl][c];
+              }
+            }
+          });
+        }
+        if (have_next) {
+          sfor<SL>([&](auto ss) {
+            constexpr int sl = decltype(ss)::value;
+            const int p = tid + sl * NTHREADS;
+            if (p < M::PAIRS) {
+              const int r = p / TT, t = p - r * TT;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) lds[M::STG_LDS + t * M::F4 + 3 * r + c] = ckn[sl][c];
+            }
+          });
+        }
         // zero the padded rows of the final-layer gradient slots
         if constexpr (M::HAS_P) {
           constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
@@ -908,19 +994,22 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 
         UDE_STAMP(pf, 12);
       }
-      #pragma unroll 1
-      for (int p = tid; p < M::PAIRS; p += NTHREADS) {
-        const int r = p / TT, t = p - r * TT;
-        float* rec = lds + t * SR;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const int f = 3 * r + c;
-          rec[M::RK_A + f] = rec[M::RK_ACCY + f] + rec[M::RK_PEND + f];
+      // step end (same thread <-> element mapping as the step start: no barrier)
+      {
+        constexpr int NV = M::F4 / 4;
+        #pragma unroll 1
+        for (int i = tid; i < TT * NV; i += NTHREADS) {
+          const int t = i / NV, v = i - t * NV;
+          float* rec = lds + t * SR + 4 * v;
+          *reinterpret_cast<f4*>(rec + M::RK_A) =
+              *reinterpret_cast<const f4*>(rec + M::RK_ACCY) + *reinterpret_cast<const f4*>(rec + M::RK_PEND);
         }
       }
+      UDE_STAMP(pf, 13);
     }
 
     // ---- tile end: dy0 (dynamic), static-feature gradients, layer-0 bias sums ----
+    __syncthreads();
     #pragma unroll 1
     for (int p = tid; p < M::PAIRS; p += NTHREADS) {
       const int r = p / TT, t = p - r * TT;
@@ -1068,46 +1157,78 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
 // ============================================================================
 // Deterministic reductions over the per-workgroup partials
 // ============================================================================
+// Slab offset -> index into the torch-ordered parameter vector (-1: padding).
+// Inverse of the dW tile layout: tile T = dyn_tiles_before(d, k) + ct holds rows
+// frt(d, k) * 16 + [0, 16) of layer d of net fnet(d, k) and input columns ct * 16 +
+// [0, 16) in MFMA C order (lane = (row >> 2) * 16 + col, reg = row & 3).
 template <class M>
-__global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __restrict__ slab, int ngrid,
-                                                                float* __restrict__ dparams) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= M::N_PARAMS) return;
-  int off = -1;
-  sfor<2>([&](auto nn) {
-    constexpr int net = decltype(nn)::value;
-    sfor<5>([&](auto ii) {
+__device__ __forceinline__ int slab_to_param(int off) {
+  int e = -1;
+  if (off >= M::SLAB_DB) {
+    const int idx = off - M::SLAB_DB, T = idx >> 4, row = idx & 15;
+    sfor<M::D>([&](auto ii) {
       constexpr int i = decltype(ii)::value;
-      if constexpr (M::has(net, i)) {
-        constexpr int in_full = i == 0 ? M::R * M::L : M::in_dim(net, i);
-        constexpr int out = M::out_dim(net, i);
-        constexpr int w0 = M::param_w_off(net, i);
-        constexpr int b0 = w0 + out * in_full;
-        constexpr int kbase = net == 0 ? 0 : M::rto(0, i);
-        if (e >= w0 && e < b0) {
-          const int o = (e - w0) / in_full, col = (e - w0) - o * in_full;
-          const int k = kbase + o / 16, row = o % 16;
-          int f = col;
-          bool stat = false;
-          if (i == 0) {
-            const int r = col / M::L, c = col - r * M::L;
-            if (c < 3) f = 3 * r + c;
-            else { f = r * (M::L - 3) + (c - 3); stat = true; }
+      if (T >= M::FTbase(i) && T < M::FTbase(i) + M::FT(i)) {
+        const int k = T - M::FTbase(i);
+        sfor<2>([&](auto nn) {
+          constexpr int net = decltype(nn)::value;
+          if constexpr (M::has(net, i)) {
+            constexpr int kb = net == 0 ? 0 : M::rto(0, i);
+            constexpr int in_full = i == 0 ? M::R * M::L : M::in_dim(net, i);
+            if (k >= kb && k < kb + M::rto(net, i)) {
+              const int o = (k - kb) * 16 + row;
+              if (o < M::out_dim(net, i)) e = M::param_w_off(net, i) + M::out_dim(net, i) * in_full + o;
+            }
           }
-          const int lane = (row >> 2) * 16 + (f & 15), reg = row & 3;
-          if (!stat) off = (M::dyn_tiles_before(i, k) + f / 16) * 256 + lane * 4 + reg;
-          else off = -2;   // static column: written by ude_static_reduce_kernel
-        } else if (e >= b0 && e < b0 + out) {
-          const int o = e - b0;
-          off = M::SLAB_DB + (M::FTbase(i) + kbase + o / 16) * 16 + (o % 16);
+        });
+      }
+    });
+    return e;
+  }
+  const int T = off >> 8, wq = off & 255, ln = wq >> 2;
+  const int row = (ln >> 4) * 4 + (wq & 3), fc = ln & 15;
+  sfor<M::D>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    sfor<M::FT(i)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      constexpr int net = M::fnet(i, k);
+      constexpr int t0 = M::dyn_tiles_before(i, k);
+      if (T >= t0 && T < t0 + M::rti(net, i)) {
+        const int f = (T - t0) * 16 + fc;
+        const int o = M::frt(i, k) * 16 + row;
+        constexpr int in_full = i == 0 ? M::R * M::L : M::in_dim(net, i);
+        if (o < M::out_dim(net, i) && f < M::in_dim(net, i)) {
+          const int col = i == 0 ? (f / 3) * M::L + (f % 3) : f;
+          e = M::param_w_off(net, i) + o * in_full + col;
         }
       }
     });
   });
-  if (off < 0) return;
-  float s = 0.f;
-  for (int gi = 0; gi < ngrid; ++gi) s += slab[(size_t)gi * M::SLAB_TOTAL + off];
-  dparams[e] = s;
+  return e;
+}
+
+// Deterministic cross-workgroup reduction of the gradient slabs: a block owns 64
+// consecutive slab offsets (coalesced reads) x 4 groups of slabs, each summed in
+// slab order, then combined in a fixed order; the result is scattered to torch order.
+template <class M>
+__global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __restrict__ slab, int ngrid,
+                                                                float* __restrict__ dparams) {
+  __shared__ float part[4][64];
+  const int lo = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int off = blockIdx.x * 64 + lo;
+  float v = 0.f;
+  if (off < M::SLAB_TOTAL) {
+    const int per = (ngrid + 3) / 4, g0 = grp * per, g1 = min(ngrid, g0 + per);
+    const float* p = slab + off;
+#pragma unroll 8
+    for (int gi = g0; gi < g1; ++gi) v += p[(size_t)gi * M::SLAB_TOTAL];
+  }
+  part[grp][lo] = v;
+  __syncthreads();
+  if (grp == 0 && off < M::SLAB_TOTAL) {
+    const int e = slab_to_param<M>(off);
+    if (e >= 0) dparams[e] = (part[0][lo] + part[1][lo]) + (part[2][lo] + part[3][lo]);
+  }
 }
 
 // ============================================================================
@@ -1116,32 +1237,58 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
 //   dy0[n][static s] = sum_o W0[o][static s] * G0[n][o] + sum_j dlatent[j][n][static s]
 // with G0[n][o] = sum over every evaluation of the layer-0 output gradient.
 // ============================================================================
+// dW0[:, static] split-K partials on MFMA: part[chunk][K0][S16] = sum over the
+// chunk's tiles of G0[tile] (K0 x 16 trajectories) x X_static[tile] (16 x S16).
+// Wave w owns static column tiles w, w + 4, ...; MFMA q covers trajectories 4g + q.
 template <class M>
 __global__ __launch_bounds__(256) void ude_static_partial_kernel(const float* __restrict__ g0buf,
                                                                  const float* __restrict__ y0, int n_traj,
                                                                  int n_tiles, float* __restrict__ part) {
-  __shared__ float sg[TT][16 + 1], sx[TT][16 + 1];
-  const int ot = blockIdx.x, st = blockIdx.y, chunk = blockIdx.z;
-  const int tid = threadIdx.x, oo = tid >> 4, ss = tid & 15;
+  constexpr int NOT = M::K0 / 16, NST = M::S16 / 16, SPW = (NST + 3) / 4;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int chunk = blockIdx.x;
   const int per = (n_tiles + M::STATIC_CHUNKS - 1) / M::STATIC_CHUNKS;
-  const int t_beg = chunk * per, t_end = min(n_tiles, t_beg + per);
-  float acc = 0.f;
-  for (int tile = t_beg; tile < t_end; ++tile) {
-    // G0 tile [16 rows][16 trajectories] and the matching static inputs [16 traj][16 feats]
-    sg[ss][oo] = g0buf[((size_t)tile * M::K0 + ot * 16 + oo) * TT + ss];
-    const int n = tile * TT + oo, sfeat = st * 16 + ss;
-    float xv = 0.f;
-    if (n < n_traj && sfeat < M::S) {
-      const int r = sfeat / (M::L - 3), c = 3 + sfeat - r * (M::L - 3);
-      xv = y0[((size_t)n * M::R + r) * M::L + c];
-    }
-    sx[oo][ss] = xv;
-    __syncthreads();
+  const int tb = chunk * per, te = min(n_tiles, tb + per);
+  f4 acc[NOT][SPW];
 #pragma unroll
-    for (int t = 0; t < TT; ++t) acc += sg[t][oo] * sx[t][ss];
-    __syncthreads();
+  for (int o = 0; o < NOT; ++o)
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) acc[o][j] = f4zero();
+  #pragma unroll 1
+  for (int tile = tb; tile < te; ++tile) {
+    f4 a[NOT];
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+      a[o] = *reinterpret_cast<const f4*>(g0buf + ((size_t)tile * M::K0 + o * 16 + t) * TT + 4 * g);
+    float b[SPW][4];
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      const int s = (w + 4 * j) * 16 + t;
+      const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = tile * TT + 4 * g + q;
+        b[j][q] = (s < M::S && n < n_traj) ? y0[((size_t)n * M::R + r) * M::L + 3 + cc] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < SPW; ++j)
+        if (w + 4 * j < NST)
+#pragma unroll
+          for (int o = 0; o < NOT; ++o) acc[o][j] = mfma4(a[o][q], b[j][q], acc[o][j]);
   }
-  part[((size_t)chunk * M::K0 + ot * 16 + oo) * M::S16 + st * 16 + ss] = acc;
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) {
+    const int st = w + 4 * j;
+    if (st >= NST) continue;
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        part[((size_t)chunk * M::K0 + o * 16 + 4 * g + e) * M::S16 + st * 16 + t] = acc[o][j][e];
+  }
 }
 
 template <class M>
@@ -1163,38 +1310,62 @@ __global__ __launch_bounds__(256) void ude_static_reduce_kernel(const float* __r
   dparams[w0 + (size_t)o * M::R * M::L + static_col<M>(s)] = v;
 }
 
+// d y0[:, static] = G0[tile]^T (16 x K0) x W0SP (K0 x S16) on MFMA, plus the direct
+// cotangents of every output time (static latent dims are carried unchanged).
+// One workgroup per trajectory tile; wave w owns static column tiles w, w + 4, ...
 template <class M>
 __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __restrict__ g0buf,
                                                              const float* __restrict__ pack,
                                                              const float* __restrict__ dlatent, int n_traj,
                                                              int n_times, float* __restrict__ dy0) {
-  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (size_t)n_traj * M::S) return;
-  const int n = (int)(idx / M::S), s = (int)(idx - (size_t)n * M::S);
-  const int tile = n / TT, tt = n - tile * TT;
-  const float* g = g0buf + (size_t)tile * M::K0 * TT + tt;
-  const float* w = pack + M::W0SP_OFF + s;
-  float v = 0.f;
+  constexpr int NST = M::S16 / 16, SPW = (NST + 3) / 4;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x;
+  const float* gb = g0buf + (size_t)tile * M::K0 * TT;
+  const float* wp = pack + M::W0SP_OFF;
+  f4 acc[SPW];
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) acc[j] = f4zero();
 #pragma unroll 8
-  for (int o = 0; o < M::K0; ++o) v += w[o * M::S16] * g[o * TT];
-  const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
-  const size_t base = ((size_t)n * M::R + r) * M::L + c;
+  for (int q = 0; q < M::K0 / 4; ++q) {
+    const float a = gb[(4 * q + g) * TT + t];          // A[traj t][o = 4q + g]
+#pragma unroll
+    for (int j = 0; j < SPW; ++j)
+      if (w + 4 * j < NST) acc[j] = mfma4(a, wp[(4 * q + g) * M::S16 + (w + 4 * j) * 16 + t], acc[j]);
+  }
   const size_t NRL = (size_t)n_traj * M::R * M::L;
-  for (int j = 0; j < n_times; ++j) v += dlatent[(size_t)j * NRL + base];
-  dy0[base] = v;
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) {
+    const int s = (w + 4 * j) * 16 + t;
+    if (w + 4 * j >= NST || s >= M::S) continue;
+    const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = tile * TT + 4 * g + e;
+      if (n >= n_traj) continue;
+      const size_t base = ((size_t)n * M::R + r) * M::L + 3 + cc;
+      float v = acc[j][e];
+      for (int jt = 0; jt < n_times; ++jt) v += dlatent[(size_t)jt * NRL + base];
+      dy0[base] = v;
+    }
+  }
 }
 
 template <int V_ = 0>
 __global__ void ude_stats_finalize_kernel(const double* __restrict__ slab, int ngrid, double n_eval,
                                           float* __restrict__ out) {
+  // wave c sums statistic c: lane-strided partials, then a fixed butterfly (deterministic)
   __shared__ double tot[5];
-  const int c = threadIdx.x;
-  if (c < 5) {
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (wv < 5) {
     double s = 0.0;
-    for (int gi = 0; gi < ngrid; ++gi) s += slab[(size_t)gi * 5 + c];
-    tot[c] = s;
+    for (int gi = ln; gi < ngrid; gi += 64) s += slab[(size_t)gi * 5 + wv];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (ln == 0) tot[wv] = s;
   }
   __syncthreads();
+  const int c = threadIdx.x;
   if (c < 2) {
     const double m = tot[c] / n_eval;
     const double var = (tot[2 + c] - n_eval * m * m) / (n_eval - 1.0);

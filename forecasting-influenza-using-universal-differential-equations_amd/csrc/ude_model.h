@@ -117,7 +117,11 @@ struct Model {
   static constexpr int LDS_F = TT * SR_F * 4;
   // + per-workgroup bias-gradient row sums (one float per forward row tile row)
   static constexpr int DB_LDS = TT * SR_B;
-  static constexpr int LDS_B = (TT * SR_B + 16 * FTbase_total()) * 4;
+  // + staging slot for the next stage's checkpointed input ([t][F4], prefetched
+  // during the flux pass)
+  static constexpr int STG_LDS = DB_LDS + 16 * FTbase_total();
+  static constexpr int LDS_B = (STG_LDS + TT * F4) * 4;
+  static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");
 
   // ---- packed weights (fragment order, 16-B per lane per MFMA quad) --------------
   //  WF(net,i): [rto][kin/16][64 lanes][4]   A operand of the forward GEMM
@@ -164,7 +168,7 @@ struct Model {
   static constexpr int SLAB_TOTAL = SLAB_DB + FTbase(D) * 16;
   // static-feature gradient work (outside the main kernel): per-tile layer-0 row sums
   // G0[tile][K0][16] and split-K partials of dW0[:, static]
-  static constexpr int STATIC_CHUNKS = 16;
+  static constexpr int STATIC_CHUNKS = 128;
 
   // ---- per-wave register tiles -----------------------------------------------------
   static constexpr int ndw_before(int w, int d, int k) {

@@ -18,9 +18,9 @@ pkg = importlib.import_module("forecasting-influenza-using-universal-differentia
 from ude_amd import _native  # noqa: E402
 import bench  # noqa: E402
 
-SEG = {0: "ckpt load (+outputs)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1", 4: "fwd d2", 5: "fwd d3",
+SEG = {0: "stage input (ckpt)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1", 4: "fwd d2", 5: "fwd d3",
        6: "flux bwd", 11: "barrier after flux", 10: "bwd d3", 9: "bwd d2", 8: "bwd d1", 7: "bwd d0",
-       12: "RK adjoint"}
+       12: "RK adjoint", 13: "step end (RK_A)", 14: "step start (cotangents)", 15: "tile start/end"}
 
 
 def main():
@@ -48,7 +48,7 @@ def main():
     per = used.mean(0) / stages
     tot = float(per.sum())
     print(f"workgroups {used.shape[0]}, stages per WG {stages:.1f}, cycles per stage {tot:.0f}")
-    for k in sorted(SEG, key=lambda s: [0, 1, 2, 3, 4, 5, 6, 11, 10, 9, 8, 7, 12].index(s)):
+    for k in sorted(SEG, key=lambda s: [15, 14, 0, 1, 2, 3, 4, 5, 6, 11, 10, 9, 8, 7, 12, 13].index(s)):
         print(f"  {SEG[k]:24s} {float(per[k]):9.0f}  {100 * float(per[k]) / tot:5.1f}%")
 
 

@@ -87,6 +87,17 @@ def build(pkg, w, device, seed):
     return mod, y0, t, dlat
 
 
+_COTS = {}
+
+
+def _cot(vals, device):
+    """Fixed loss cotangents (created once: they stand for upstream gradients)."""
+    key = (tuple(vals) if isinstance(vals, (list, tuple)) else vals, str(device))
+    if key not in _COTS:
+        _COTS[key] = torch.tensor(vals, device=device)
+    return _COTS[key]
+
+
 def one_step(pkg, udist, mod, y0, t, dlat, world):
     mod.clear_tracking()
     mod.zero_grad(set_to_none=True)
@@ -98,10 +109,10 @@ def one_step(pkg, udist, mod, y0, t, dlat, world):
     if mod.ode_type in ("Fp", "FaFp"):
         post = mod.posterior()
         outs += [post.loc, post.scale]
-        cots += [torch.tensor([0.3, -0.2], device=y0.device), torch.tensor([0.5, 0.1], device=y0.device)]
+        cots += [_cot([0.3, -0.2], y0.device), _cot([0.5, 0.1], y0.device)]
     if mod.ode_type in ("Fa", "FaFp"):
         outs.append(torch.norm(torch.stack(mod.tracker)))
-        cots.append(torch.tensor(0.1, device=y0.device))
+        cots.append(_cot(0.1, y0.device))
     torch.autograd.backward(outs, cots)
     if world > 1:
         udist.all_reduce_grads(mod.parameters())

@@ -174,8 +174,16 @@ using C1Arr = f4[NZ_ > 0 ? NZ_ : 1];
 // Forward pass of both MLPs for the stage input held in the record's Y slot.
 // Leaves post-activation outputs of every layer in the record (the final
 // layers' raw outputs: P-net pre-|.| rates q, A-net Fa).  Ends on a barrier.
-template <class M, int W, int SR>
-__device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, int lane, Prof* pf = nullptr) {
+struct NoHook {
+  template <class D>
+  __device__ __forceinline__ void operator()(D) const {}
+};
+
+// `hook(integral_constant<d>)` runs right after phase d's weight loads are issued
+// (used by the backward to start HBM loads early without holding registers long).
+template <class M, int W, int SR, class Hook = NoHook>
+__device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, int lane, Prof* pf = nullptr,
+                                            const Hook& hook = Hook{}) {
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto dd) {
@@ -192,6 +200,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
         if constexpr (!(d == 0 && M::S > 0)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
       }
     });
+    hook(dd);
     __builtin_amdgcn_sched_barrier(0);
     f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
     sfor<M::FT(d)>([&](auto kk) {
@@ -624,10 +633,32 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
 // Cotangents of the outputs written after RK step `step` (torchdiffeq's
 // _linear_interp between y_step and y_step+1): sg = the y_{step+1}-side share,
 // pg = the y_step-side share, per pair slot (p = tid + sl * NTHREADS) and S/I/R.
+// out_issue starts the loads of the step's first output (if any); out_finish turns
+// them into shares and handles any further outputs of the step synchronously.
 template <class M>
-__device__ __forceinline__ void out_shares(const KArgs& A, const Sched& sc, int step, int n0,
-                                           float (&sg)[M::SLOTS][3], float (&pg)[M::SLOTS][3]) {
+__device__ __forceinline__ void out_load(const KArgs& A, const Sched& sc, int o, int n0,
+                                         float (&gv)[M::SLOTS][3]) {
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL;
+  sfor<M::SLOTS>([&](auto ss) {
+    constexpr int sl = decltype(ss)::value;
+    const int p = threadIdx.x + sl * NTHREADS;
+    const int r = p / TT, t = p - r * TT, n = n0 + t;
+    const bool valid = p < M::PAIRS && n < A.n_traj;
+    const size_t base = valid ? ((size_t)n * M::R + r) * M::L : 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gv[sl][c] = valid ? gl[base + c] : 0.f;
+  });
+}
+template <class M>
+__device__ __forceinline__ void out_issue(const KArgs& A, const Sched& sc, int step, int n0,
+                                          float (&gv)[M::SLOTS][3]) {
+  if (sc.out_start[step] < sc.out_start[step + 1]) out_load<M>(A, sc, sc.out_start[step], n0, gv);
+}
+template <class M>
+__device__ __forceinline__ void out_finish(const KArgs& A, const Sched& sc, int step, int n0,
+                                           float (&gv)[M::SLOTS][3], float (&sg)[M::SLOTS][3],
+                                           float (&pg)[M::SLOTS][3]) {
 #pragma unroll
   for (int sl = 0; sl < M::SLOTS; ++sl)
 #pragma unroll
@@ -635,19 +666,9 @@ __device__ __forceinline__ void out_shares(const KArgs& A, const Sched& sc, int 
   const int o_beg = sc.out_start[step], o_end = sc.out_start[step + 1];
   #pragma unroll 1
   for (int o = o_beg; o < o_end; ++o) {
+    if (o > o_beg) out_load<M>(A, sc, o, n0, gv);
     const int mode = sc.out_mode[o];
     const float slope = sc.out_slope[o];
-    const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL;
-    float gv[M::SLOTS][3];
-    sfor<M::SLOTS>([&](auto ss) {
-      constexpr int sl = decltype(ss)::value;
-      const int p = threadIdx.x + sl * NTHREADS;
-      const int r = p / TT, t = p - r * TT, n = n0 + t;
-      const bool valid = p < M::PAIRS && n < A.n_traj;
-      const size_t base = valid ? ((size_t)n * M::R + r) * M::L : 0;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) gv[sl][c] = valid ? gl[base + c] : 0.f;
-    });
 #pragma unroll
     for (int sl = 0; sl < M::SLOTS; ++sl)
 #pragma unroll
@@ -846,17 +867,21 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
     load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
-    #pragma unroll 1
-    for (int i = tid; i < TT * M::F; i += NTHREADS) {
-      const int t = i / M::F;
-      lds[t * SR + M::RK_A + (i - t * M::F)] = 0.f;
-    }
     // output cotangents of the last step: y_{n+1} share -> RK_A, y_n share staged in
     // DK3 (picked up by the step start).  Later steps get theirs under the flux pass
-    // of the previous step's last stage.
-    if (A.n_steps > 0) {
-      float sg[SL][3], pg[SL][3];
-      out_shares<M>(A, sc, A.n_steps - 1, n0, sg, pg);
+    // of the previous step's last stage.  (These pair-mapped stores are the only
+    // writes of RK_A here: every (t, f < F) is covered, zeros without a step.)
+    {
+      float gv[SL][3], sg[SL][3], pg[SL][3];
+      if (A.n_steps > 0) {
+        out_issue<M>(A, sc, A.n_steps - 1, n0, gv);
+        out_finish<M>(A, sc, A.n_steps - 1, n0, gv, sg, pg);
+      } else {
+#pragma unroll
+        for (int sl = 0; sl < SL; ++sl)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) { sg[sl][c] = 0.f; pg[sl][c] = 0.f; }
+      }
       sfor<SL>([&](auto ss) {
         constexpr int sl = decltype(ss)::value;
         const int p = tid + sl * NTHREADS;
@@ -929,21 +954,27 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 0);
         __syncthreads();
         UDE_STAMP(pf, 1);
-        mlp_forward<M, W, SR>(rs, lds, c1, lane, pf);
+        // at the step's last stage the next step's output cotangents are loaded from
+        // fwd phase 1 on (consumed after the flux pass)
+        const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
+        have_next = nstep >= 0;
+        const bool next_out = jj == 0 && have_next;
+        float gvn[SL][3];
+        mlp_forward<M, W, SR>(rs, lds, c1, lane, pf, [&](auto dd) {
+          if constexpr (decltype(dd)::value == (M::D > 2 ? 1 : 0))
+            if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+        });
 
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
         // the next stage's checkpointed input is fetched under the flux pass and the
         // MLP backward (registers only live across the flux pass)
-        const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
-        have_next = nstep >= 0;
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         if (have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        const bool next_out = jj == 0 && have_next;
-        if (next_out) out_shares<M>(A, sc, nstep, n0, sgn, pgn);
         flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         if (next_out) {
+          out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
           sfor<SL>([&](auto ss) {
@@ -1339,15 +1370,24 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
     const int s = (w + 4 * j) * 16 + t;
     if (w + 4 * j >= NST || s >= M::S) continue;
     const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
+    // the 4 trajectories' cotangent streams are summed side by side (time order per
+    // element); unrolled so a few dozen HBM loads are in flight per lane
+    size_t base[4];
+    f4 v = acc[j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int n = tile * TT + 4 * g + e;
-      if (n >= n_traj) continue;
-      const size_t base = ((size_t)n * M::R + r) * M::L + 3 + cc;
-      float v = acc[j][e];
-      for (int jt = 0; jt < n_times; ++jt) v += dlatent[(size_t)jt * NRL + base];
-      dy0[base] = v;
+      const int n = min(tile * TT + 4 * g + e, n_traj - 1);
+      base[e] = ((size_t)n * M::R + r) * M::L + 3 + cc;
     }
+#pragma unroll 4
+    for (int jt = 0; jt < n_times; ++jt) {
+      const float* dl = dlatent + (size_t)jt * NRL;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += dl[base[e]];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (tile * TT + 4 * g + e < n_traj) dy0[base[e]] = v[e];
   }
 }
 

@@ -18,6 +18,7 @@ Adaptive methods (dopri5, ...) are recognised but not implemented yet.
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from typing import Optional
 
 import torch
@@ -51,14 +52,55 @@ def fusable(func, y0: torch.Tensor) -> bool:
             and all(p.is_cuda and p.dtype == torch.float32 for p in func.parameters()))
 
 
+# Host-side caches so that a training loop calling odeint with the same time grid
+# does not round-trip t through the host (and re-upload the schedule) every call.
+# t is keyed by identity + in-place version (a strong reference is kept, so the id
+# cannot be reused while cached); plans by the grid's values.
+_T_CACHE: "OrderedDict" = OrderedDict()
+_PLAN_CACHE: "OrderedDict" = OrderedDict()
+_CACHE_MAX = 16
+
+
+def _lru_put(cache, key, value):
+    cache[key] = value
+    cache.move_to_end(key)
+    while len(cache) > _CACHE_MAX:
+        cache.popitem(last=False)
+
+
+def _host_t(t: torch.Tensor) -> torch.Tensor:
+    """Validated host copy of t (torchdiffeq's checks), cached per tensor version."""
+    key = (id(t), t._version)
+    hit = _T_CACHE.get(key)
+    if hit is not None and hit[0] is t:
+        return hit[1]
+    host = t.detach().cpu()
+    _check_t(host)
+    _lru_put(_T_CACHE, key, (t, host))
+    return host
+
+
 def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=None) -> torch.Tensor:
-    sched = build_schedule(t, step_size)
+    th = _host_t(t)
+    if isinstance(step_size, torch.Tensor):
+        step_size = step_size.detach().cpu()
+    step_key = None if step_size is None else (
+        step_size.to(th.dtype).numpy().tobytes() if isinstance(step_size, torch.Tensor) else float(step_size))
     lins = func.ude_linears()
     params = []
     for lin in lins:
         params += [lin.weight, lin.bias]
-    plan = _fused.make_plan(func.ude_config(), sched, y0.shape[0], func.fa_weight(), y0.device,
-                            [p.shape for p in params])
+    cfg = func.ude_config()
+    fa_w = func.fa_weight()
+    key = (cfg, str(th.dtype), th.numpy().tobytes(), step_key, int(y0.shape[0]), float(fa_w), str(y0.device),
+           tuple(tuple(p.shape) for p in params))
+    plan = _PLAN_CACHE.get(key)
+    if plan is None:
+        sched = build_schedule(th, step_size)
+        plan = _fused.make_plan(cfg, sched, y0.shape[0], fa_w, y0.device, [p.shape for p in params])
+        _lru_put(_PLAN_CACHE, key, plan)
+    else:
+        _PLAN_CACHE.move_to_end(key)
     latent, stats = _fused.FusedRK4.apply(plan, y0.contiguous(), *params)
     func._record_fused(stats, plan.n_eval)
     return latent
@@ -114,7 +156,10 @@ def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, even
     if method not in FIXED_METHODS + ADAPTIVE_METHODS:
         raise ValueError('Invalid method "{}". Must be one of {}'.format(
             method, '{"' + '", "'.join(FIXED_METHODS + ADAPTIVE_METHODS) + '"}.'))
-    _check_t(t)
+    if torch.is_tensor(t) and t.is_cuda and method == "rk4":
+        _host_t(t)           # validated once per tensor version, no device sync when cached
+    else:
+        _check_t(t)
     options = dict(options or {})
     step_size = options.pop("step_size", None)
     if method in ADAPTIVE_METHODS:

@@ -192,3 +192,22 @@ def test_full_size_properties(pkg):
     assert torch.equal(sub, lat[:, :64])
     # static latent dims are carried unchanged
     assert torch.equal(lat[:, :, :, 3:], y0[None, :, :, 3:].expand_as(lat[:, :, :, 3:]))
+
+
+@pytest.mark.gpu
+def test_cached_grid_follows_inplace_updates(pkg):
+    """The host-side t / plan caches must not serve a stale schedule when the same
+    device tensor t is modified in place between solves."""
+    mod, y0, t, h, dl = _random_case(pkg, "FaFp", 1, 8, [64, 64, 32], [64, 64], 16, 6, 7.0, "t1-t0")
+    ref = OracleRHS.from_module(mod, torch.float64)
+    mg = mod.to(DEV)
+    td = t.to(DEV)
+    for scale in (1.0, 2.0):
+        if scale != 1.0:
+            td.mul_(scale)                       # same tensor object, new values
+        tc = td.cpu()
+        want = solve_and_grad(ref, y0.double(), tc, tc[1] - tc[0]).latent
+        mg.clear_tracking()
+        with torch.no_grad():
+            lat = pkg.odeint(mg, y0.to(DEV), td, method="rk4", options=dict(step_size=td[1] - td[0]))
+        assert normwise_rel(lat, want) < 1e-5, scale

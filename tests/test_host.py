@@ -137,3 +137,15 @@ def test_registry_has_every_prebuilt_config(native):
         assert lib.supported(native.make_desc(cfg)), cfg
     assert not lib.supported(native.make_desc(("FaFp", 7, 8, (13,), (11,))))
     assert "gfx950" in lib.build_info()
+
+
+def test_host_t_cache_tracks_inplace_updates(pkg):
+    """odeint's host copy of t is cached per tensor version: an in-place update is
+    seen (here it makes t non-increasing, which must raise like torchdiffeq)."""
+    from ude_amd import solvers
+    t = torch.arange(6, dtype=torch.float32)
+    h1 = solvers._host_t(t)
+    assert solvers._host_t(t) is h1            # cached
+    t[3] = 0.0
+    with pytest.raises(AssertionError):
+        solvers._host_t(t)

@@ -14,6 +14,7 @@ extern unsigned long long* g_prof_buffer;   // diagnostic builds: set by ude_deb
 
 template <class M>
 bool matches(const UdeModelDesc* d) {
+  if (!M::FITS) return false;
   if (d->kind != M::KIND || d->n_regions != M::R || d->latent_dim != M::L) return false;
   if (M::HAS_P) {
     if (d->n_p_hidden != M::NPH) return false;
@@ -58,24 +59,30 @@ struct Ops {
     return UDE_OK;
   }
 
-  // grad-slab workspace tail: G0 [tile][K0][16] + split-K partials [chunks][K0][S16]
+  // grad-slab workspace tail (HOIST): G0 [tile][K0][16] + split-K partials [chunks][K0][S16]
   static int64_t static_ws_floats(int n_tiles) {
-    if (M::S == 0) return 0;
+    if (!M::HOIST) return 0;
     return (int64_t)n_tiles * M::K0 * TT + (int64_t)M::STATIC_CHUNKS * M::K0 * M::S16;
   }
 
+  // BAYES: one weight sample per RHS evaluation (4 per RK4 step)
+  static int64_t n_evals(const UdeProblem* p) { return M::BAYES ? 4 * (int64_t)p->n_steps : 1; }
+
   static int query(const UdeProblem* p, int device, UdeSizes* o) {
     if (p->n_traj < 1 || p->n_steps < 0 || p->n_out < 0) return UDE_E_INVALID;
+    if (M::BAYES && 4 * (int64_t)p->n_steps > 65535) return UDE_E_INVALID;   // grid.y / grid.z of the packers
     const int n_tiles = (p->n_traj + TT - 1) / TT;
     int gf = 1, gb = 1;
     int rc = grids(device, n_tiles, &gf, &gb);
     if (rc) return rc;
-    o->pack_bytes = (int64_t)M::PACK_TOTAL * 4;
+    const int64_t ne = n_evals(p) > 0 ? n_evals(p) : 1;
+    // BAYES: [eval][PACK_TOTAL] weight samples, then [eval][SLAB_TOTAL] eps in slab order
+    o->pack_bytes = M::BAYES ? ne * (int64_t)(M::PACK_TOTAL + M::SLAB_TOTAL) * 4 : (int64_t)M::PACK_TOTAL * 4;
     o->sched_bytes = (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
     o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * M::F * TT * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
-    o->grad_slab_bytes = (int64_t)gb * M::SLAB_TOTAL * 4 + static_ws_floats(n_tiles) * 4;
-    o->n_params = M::N_PARAMS;
+    o->grad_slab_bytes = (int64_t)gb * M::SLAB_STRIDE * 4 + static_ws_floats(n_tiles) * 4;
+    o->n_params = M::N_GRAD;
     o->grid_fwd = gf;
     o->grid_bwd = gb;
     o->lds_fwd = M::LDS_F;
@@ -83,16 +90,7 @@ struct Ops {
     return UDE_OK;
   }
 
-  static int pack(const float* const* W, const float* const* b, float* out, hipStream_t s) {
-    PackPtrs P;
-    memset(&P, 0, sizeof(P));
-    int li = 0;
-    for (int net = 0; net < 2; ++net)
-      for (int i = 0; i < M::nl(net); ++i, ++li) {
-        if (!W[li] || !b[li]) return UDE_E_INVALID;
-        P.W[net][i] = W[li];
-        P.b[net][i] = b[li];
-      }
+  static int launch_pack(const PackPtrs& P, float* out, int n_ev, hipStream_t s) {
     int mx = M::W0SP_SIZE;
     for (int net = 0; net < 2; ++net) {
       if (M::wsf_size(net) > mx) mx = M::wsf_size(net);
@@ -102,8 +100,48 @@ struct Ops {
         if (M::b_size(net, i) > mx) mx = M::b_size(net, i);
       }
     }
-    dim3 grid((mx + 255) / 256, 33);
+    dim3 grid((mx + 255) / 256, 33, n_ev);
     hipLaunchKernelGGL(ude_pack_kernel<M>, grid, dim3(256), 0, s, P, out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  static int pack(const float* const* W, const float* const* b, float* out, hipStream_t s) {
+    if (M::BAYES) return UDE_E_INVALID;          // ude_pack_weights_bayes
+    PackPtrs P;
+    memset(&P, 0, sizeof(P));
+    int li = 0;
+    for (int net = 0; net < 2; ++net)
+      for (int i = 0; i < M::nl(net); ++i, ++li) {
+        if (!W[li] || !b[li]) return UDE_E_INVALID;
+        P.W[net][i] = W[li];
+        P.b[net][i] = b[li];
+      }
+    return launch_pack(P, out, 1, s);
+  }
+
+  static int pack_bayes(const UdeProblem* p, const float* const* W, const float* const* b, const float* const* Ws,
+                        const float* const* bs, const float* eps, float* out, hipStream_t s) {
+    if (!M::BAYES) return UDE_E_INVALID;         // ude_pack_weights
+    if (!eps || p->n_steps < 0 || 4 * (int64_t)p->n_steps > 65535) return UDE_E_INVALID;
+    const int ne = (int)n_evals(p);
+    if (ne == 0) return UDE_OK;                  // no evaluation, nothing to pack
+    PackPtrs P;
+    memset(&P, 0, sizeof(P));
+    int li = 0;
+    for (int net = 0; net < 2; ++net)
+      for (int i = 0; i < M::nl(net); ++i, ++li) {
+        if (!W[li] || !b[li] || !Ws[li] || !bs[li]) return UDE_E_INVALID;
+        P.W[net][i] = W[li];
+        P.b[net][i] = b[li];
+        P.Ws[net][i] = Ws[li];
+        P.bs[net][i] = bs[li];
+      }
+    P.eps = eps;
+    int rc = launch_pack(P, out, ne, s);
+    if (rc) return rc;
+    float* eslab = out + (size_t)ne * M::PACK_TOTAL;
+    hipLaunchKernelGGL(ude_eps_slab_kernel<M>, dim3((M::SLAB_TOTAL + 255) / 256, ne), dim3(256), 0, s, eps, eslab);
     HIPCHK(hipGetLastError());
     return UDE_OK;
   }
@@ -148,7 +186,8 @@ struct Ops {
     a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
     a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.stats_out = stats_out; a.dstats = dstats;
     a.dy0 = dy0; a.slab = slab;
-    float* g0buf = slab + (size_t)gb * M::SLAB_TOTAL;
+    if (M::BAYES) a.eslab = pack + (size_t)n_evals(p) * M::PACK_TOTAL;
+    float* g0buf = slab + (size_t)gb * M::SLAB_STRIDE;
     float* part = g0buf + (size_t)n_tiles * M::K0 * TT;
     a.g0buf = g0buf;
 #ifdef UDE_PROFILE
@@ -161,7 +200,13 @@ struct Ops {
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());
-    if (M::S > 0) {
+    if (M::BAYES) {
+      // d |std|: the eps-weighted half of every workgroup slab
+      hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
+                         (const float*)(slab + M::SLAB_TOTAL), gb, dparams + M::N_PARAMS);
+      HIPCHK(hipGetLastError());
+    }
+    if (M::HOIST) {
       hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS), dim3(256), 0, s,
                          (const float*)g0buf, y0, p->n_traj, n_tiles, part);
       HIPCHK(hipGetLastError());
@@ -180,6 +225,8 @@ struct Entry {
   bool (*match)(const UdeModelDesc*);
   int (*query)(const UdeProblem*, int, UdeSizes*);
   int (*pack)(const float* const*, const float* const*, float*, hipStream_t);
+  int (*pack_bayes)(const UdeProblem*, const float* const*, const float* const*, const float* const*,
+                    const float* const*, const float*, float*, hipStream_t);
   int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*, float*, hipStream_t);
   int (*backward)(const UdeProblem*, const float*, const void*, const float*, const float*, const float*,
                   const float*, const float*, float*, float*, float*, hipStream_t);
@@ -187,7 +234,7 @@ struct Entry {
 
 template <class M>
 constexpr Entry make_entry() {
-  return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::forward, &Ops<M>::backward};
+  return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward};
 }
 
 

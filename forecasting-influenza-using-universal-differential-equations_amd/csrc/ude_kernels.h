@@ -63,6 +63,7 @@ struct KArgs {
   float fa_w;
   unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
   float* g0buf;               // backward: per-trajectory layer-0 gradient sums [tile][K0][16]
+  const float* eslab;         // BAYES backward: the eps stream in slab order, [eval][SLAB_TOTAL]
 };
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
@@ -197,7 +198,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
       if constexpr (M::fowner(d, k) == W) {
         constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
         load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
-        if constexpr (!(d == 0 && M::S > 0)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
+        if constexpr (!(d == 0 && M::HOIST)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
       }
     });
     hook(dd);
@@ -206,7 +207,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
-        if constexpr (d == 0 && M::S > 0) acc[k] = c1[M::nz_before(W, k)];
+        if constexpr (d == 0 && M::HOIST) acc[k] = c1[M::nz_before(W, k)];
         else acc[k] = bias[k];
       }
     });
@@ -260,7 +261,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
 // Static-feature hoist: c1[o][t] = b0[o] + sum_s W0[o][static s] * x_static[t][s].
 template <class M, int W, int SR, int XOFF>
 __device__ __forceinline__ void static_hoist(Rsrc rs, const float* lds, f4* c1, int lane) {
-  if constexpr (M::S > 0) {
+  if constexpr (M::HOIST) {
     const int t = lane & 15, g = lane >> 4;
     sfor<M::FT(0)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -354,7 +355,10 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     for (int step = 0; step < A.n_steps; ++step) {
       const float dt = sc.dt[step];
       for (int j = 0; j < 4; ++j) {
-        mlp_forward<M, W, SR>(rs, lds, c1, lane);
+        // BAYES: evaluation 4 step + j has its own weight sample
+        Rsrc rse = rs;
+        if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
+        mlp_forward<M, W, SR>(rse, lds, c1, lane);
         sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
@@ -484,6 +488,14 @@ struct RkAdjointEp {
   float dt;
   int jj;          // RK stage (3..0)
   __device__ __forceinline__ void operator()(int f0, f4 dY) const {
+    if constexpr (M::FULL0) {
+      // static features (rows F16..): no RK adjoint, their input gradient is summed
+      // over every evaluation of the solve (DYS, written to dy0 at tile end)
+      if (f0 >= M::F16) {
+        *reinterpret_cast<f4*>(rec + M::DYS_OFF + f0 - M::F16) += dY;
+        return;
+      }
+    }
     if (f0 >= M::F4) return;                       // padded feature rows
     f4* accy = reinterpret_cast<f4*>(rec + M::RK_ACCY + f0);
     f4* dk1 = reinterpret_cast<f4*>(rec + M::RK_DK1 + f0);
@@ -502,9 +514,12 @@ struct RkAdjointEp {
   }
 };
 
-template <class M, int W, int SR, class DW, class G0, class EP0>
-__device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0t, int lane, Prof* pf,
-                                             const EP0& ep0) {
+// BAYES: `es` addresses this evaluation's eps in slab order; every tile's dW
+// contribution of the evaluation is also accumulated eps-weighted into `dws` (and the
+// bias row sums into DBS): d|std| = sum_eval eps_eval * dW_eval (models_bayes.py:45-46).
+template <class M, int W, int SR, class DW, class DS, class G0, class EP0>
+__device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
+                                             Prof* pf, const EP0& ep0) {
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
@@ -528,6 +543,22 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
         }
       }
     });
+    // BAYES: this evaluation's eps for the wave's dW tiles (C layout) and bias rows
+    constexpr int NE = M::BAYES ? M::ndw_phase(W, d) : 0;
+    f4 ef[NE > 0 ? NE : 1], eb[M::FT(d) > 0 ? M::FT(d) : 1];
+    if constexpr (M::BAYES) {
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          constexpr int e0 = M::ndw_before(W, d, k) - M::ndw_before(W, d, 0);
+          sfor<M::rti(M::fnet(d, k), d)>([&](auto cc) {
+            constexpr int ct = decltype(cc)::value;
+            ef[e0 + ct] = ldw(es, lane * 16, (M::dyn_tiles_before(d, k) + ct) * 1024);
+          });
+          eb[k] = ldw(es, g * 16, (M::SLAB_DB + (M::FTbase(d) + k) * 16) * 4);
+        }
+      });
+    }
     __builtin_amdgcn_sched_barrier(0);
     // (1) rows owned by this wave: bias/G sums and the dW GEMM (K = trajectories)
     sfor<M::FT(d)>([&](auto kk) {
@@ -538,7 +569,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
         constexpr int goff = M::gbuf(net, d);
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
         const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
-        if constexpr (d == 0) {
+        if constexpr (d == 0 && !M::BAYES) {
           g0t[M::nz_before(W, k)] += gv;          // per-trajectory sums: static-feature gradients
         } else {
           // bias gradient: sum over the tile's 16 trajectories, then into this
@@ -552,6 +583,11 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
           if (t == 0) {
             float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
             db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+            if constexpr (M::BAYES) {
+              float* dbs = lds + M::DBS_LDS + (M::FTbase(d) + k) * 16 + g * 4;
+              const f4 e = eb[k];
+              dbs[0] += r[0] * e[0]; dbs[1] += r[1] * e[1]; dbs[2] += r[2] * e[2]; dbs[3] += r[3] * e[3];
+            }
           }
         }
         // all of the tile's LDS operands are read before its first MFMA: one LDS
@@ -565,14 +601,33 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, float* lds, DW& dw, G0& g0
           for (int ct = 0; ct < NC; ++ct) bv[s][ct] = lds[(4 * g + s) * SR + inoff + ct * 16 + t];
         }
         __builtin_amdgcn_sched_barrier(0);
-        // s outer: consecutive MFMAs update different dW tiles (no accumulator chain)
+        if constexpr (M::BAYES) {
+          // this evaluation's tile contribution on its own, then into both sums
+          f4 tmp[NC];
+          sfor<NC>([&](auto cc) { tmp[decltype(cc)::value] = f4zero(); });
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+          for (int s = 0; s < 4; ++s)
+            sfor<NC>([&](auto cc) {
+              constexpr int ct = decltype(cc)::value;
+              tmp[ct] = mfma4(ga[s], bv[s][ct], tmp[ct]);
+            });
           sfor<NC>([&](auto cc) {
             constexpr int ct = decltype(cc)::value;
             constexpr int idx = M::ndw_before(W, d, k) + ct;
-            dw[idx] = mfma4(ga[s], bv[s][ct], dw[idx]);
+            constexpr int e0 = M::ndw_before(W, d, k) - M::ndw_before(W, d, 0);
+            dw[idx] += tmp[ct];
+            dws[idx] += tmp[ct] * ef[e0 + ct];
           });
+        } else {
+          // s outer: consecutive MFMAs update different dW tiles (no accumulator chain)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            sfor<NC>([&](auto cc) {
+              constexpr int ct = decltype(cc)::value;
+              constexpr int idx = M::ndw_before(W, d, k) + ct;
+              dw[idx] = mfma4(ga[s], bv[s][ct], dw[idx]);
+            });
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     });
@@ -826,7 +881,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   const int t16 = lane & 15, g = lane >> 4;
   const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
-  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_TOTAL;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
 
   // side-statistic cotangents -> per-eval gradient coefficients
@@ -848,9 +903,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
   }
 
-  f4 dw[NDWn], g0t[NZn], c1[NZn];
+  f4 dw[NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  if constexpr (M::BAYES) {
+#pragma unroll
+    for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
+  }
   Prof prof_, *pf = nullptr;
 #ifdef UDE_PROFILE
   if (A.prof && tid == 0) {
@@ -867,6 +926,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
     load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    if constexpr (M::FULL0) {
+      #pragma unroll 1
+      for (int i = tid; i < TT * M::S16; i += NTHREADS) {
+        const int t = i / M::S16, s = i - t * M::S16;
+        lds[t * SR + M::DYS_OFF + s] = 0.f;
+      }
+    }
     // output cotangents of the last step: y_{n+1} share -> RK_A, y_n share staged in
     // DK3 (picked up by the step start).  Later steps get theirs under the flux pass
     // of the previous step's last stage.  (These pair-mapped stores are the only
@@ -960,7 +1026,14 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         have_next = nstep >= 0;
         const bool next_out = jj == 0 && have_next;
         float gvn[SL][3];
-        mlp_forward<M, W, SR>(rs, lds, c1, lane, pf, [&](auto dd) {
+        // BAYES: evaluation 4 step + jj's weight sample and eps
+        Rsrc rse = rs, es = rs;
+        if constexpr (M::BAYES) {
+          const size_t ev = (size_t)(4 * step + jj);
+          rse = make_rsrc(A.pack + ev * M::PACK_TOTAL, M::PACK_TOTAL * 4);
+          es = make_rsrc(A.eslab + ev * M::SLAB_TOTAL, M::SLAB_TOTAL * 4);
+        }
+        mlp_forward<M, W, SR>(rse, lds, c1, lane, pf, [&](auto dd) {
           if constexpr (decltype(dd)::value == (M::D > 2 ? 1 : 0))
             if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
         });
@@ -1021,7 +1094,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);
-        mlp_backward<M, W, SR>(rs, lds, dw, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj});
+        mlp_backward<M, W, SR>(rse, es, lds, dw, dws, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj});
 
         UDE_STAMP(pf, 12);
       }
@@ -1051,14 +1124,33 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         for (int c = 0; c < 3; ++c) A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] + A.dlatent[base + c];
       }
     }
+    if constexpr (M::FULL0) {
+      // static latent dims: the summed input gradient of every evaluation plus the
+      // direct cotangent of every output time (they are carried unchanged)
+      const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+      #pragma unroll 1
+      for (int i = tid; i < TT * M::S; i += NTHREADS) {
+        const int t = i / M::S, s = i - t * M::S;
+        const int n = n0 + t;
+        if (n < A.n_traj) {
+          const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
+          const size_t base = ((size_t)n * M::R + r) * M::L + c;
+          float v = lds[t * SR + M::DYS_OFF + s];
+          #pragma unroll 4
+          for (int jt = 0; jt <= A.n_out; ++jt) v += A.dlatent[(size_t)jt * NRL + base];
+          A.dy0[base] = v;
+        }
+      }
+    }
     __syncthreads();
     // per-trajectory layer-0 gradient sums -> global (static-feature gradients are
     // computed from them by ude_static_*_kernel); their trajectory sums -> bias row sums
-    sfor<M::FT(0)>([&](auto kk) {
+    // (BAYES: layer-0 bias and static columns were accumulated per evaluation instead)
+    if constexpr (!M::BAYES) sfor<M::FT(0)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(0, k) == W) {
         const f4 gv = g0t[M::nz_before(W, k)];
-        if constexpr (M::S > 0) {
+        if constexpr (M::HOIST) {
           float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
           dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
         }
@@ -1087,12 +1179,18 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         sfor<M::rti(net, d)>([&](auto cc) {
           constexpr int ct = decltype(cc)::value;
           reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
+          if constexpr (M::BAYES)
+            reinterpret_cast<f4*>(myslab + M::SLAB_TOTAL + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] =
+                dws[M::ndw_before(W, d, k) + ct];
         });
       }
     });
   });
   #pragma unroll 1
-  for (int i = tid; i < 16 * M::FTbase_total(); i += NTHREADS) myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
+  for (int i = tid; i < M::NDB; i += NTHREADS) {
+    myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
+    if constexpr (M::BAYES) myslab[M::SLAB_TOTAL + M::SLAB_DB + i] = lds[M::DBS_LDS + i];
+  }
 #ifdef UDE_PROFILE
   if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
 #endif
@@ -1114,23 +1212,26 @@ __global__ __launch_bounds__(NTHREADS) void ude_bwd_kernel(KArgs a) {
 struct PackPtrs {
   const float* W[2][5];
   const float* b[2][5];
+  const float* Ws[2][5];   // BAYES: w_std / b_std (|.| is taken here, models_bayes.py:45-46)
+  const float* bs[2][5];
+  const float* eps;        // BAYES: [eval][N_PARAMS] in torch parameter order
 };
 
-template <class M>
-__device__ __forceinline__ int in_col(int i, int f) {
-  // layer-0 dynamic feature f = 3r + c  ->  torch column r*L + c
-  return i == 0 ? (f / 3) * M::L + (f % 3) : f;
-}
 template <class M>
 __device__ __forceinline__ int static_col(int s) {
   const int r = s / (M::L - 3);
   return r * M::L + 3 + (s - r * (M::L - 3));
 }
 
+// One launch packs every segment (blockIdx.y) of one weight set; BAYES: blockIdx.z =
+// evaluation, whose sample w = mu + eps * |std| (the reference's fp32 op order) is
+// packed PACK_TOTAL floats after the previous one's.
 template <class M>
 __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __restrict__ pack) {
   const int seg = blockIdx.y;
   const int idx = blockIdx.x * 256 + threadIdx.x;
+  const size_t ev = M::BAYES ? blockIdx.z : 0;
+  pack += ev * M::PACK_TOTAL;
   sfor<2>([&](auto nn) {
     constexpr int net = decltype(nn)::value;
     sfor<5>([&](auto ii) {
@@ -1140,22 +1241,34 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
         constexpr int in = M::in_dim(net, i), out = M::out_dim(net, i);
         constexpr int in_full = i == 0 ? M::R * M::L : in;
         const float* Wp = P.W[net][i];
+        auto wval = [&](int o, int f) -> float {
+          const int col = i == 0 ? M::col0(f) : (f < in ? f : -1);
+          if (o >= out || col < 0) return 0.f;
+          const size_t w = (size_t)o * in_full + col;
+          float v = Wp[w];
+          if constexpr (M::BAYES) v = v + P.eps[ev * M::N_PARAMS + M::param_w_off(net, i) + w] * fabsf(P.Ws[net][i][w]);
+          return v;
+        };
         if (seg == base + 0 && idx < M::wf_size(net, i)) {
           constexpr int KQ = M::kin(net, i) / 4, NQ = M::kin(net, i) / 16;
           const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
-          const int o = rt * 16 + (ln & 15), f = (ln >> 4) * KQ + 4 * q + e;
-          pack[M::wf_off(net, i) + idx] = (o < out && f < in) ? Wp[(size_t)o * in_full + in_col<M>(i, f)] : 0.f;
+          pack[M::wf_off(net, i) + idx] = wval(rt * 16 + (ln & 15), (ln >> 4) * KQ + 4 * q + e);
         } else if (seg == base + 1 && idx < M::wt_size(net, i)) {
           constexpr int KQ = M::kout(net, i) / 4, NQ = M::kout(net, i) / 16;
           const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
-          const int o = (ln >> 4) * KQ + 4 * q + e, f = rt * 16 + (ln & 15);
-          pack[M::wt_off(net, i) + idx] = (o < out && f < in) ? Wp[(size_t)o * in_full + in_col<M>(i, f)] : 0.f;
+          pack[M::wt_off(net, i) + idx] = wval((ln >> 4) * KQ + 4 * q + e, rt * 16 + (ln & 15));
         } else if (seg == base + 2 && idx < M::b_size(net, i)) {
-          pack[M::b_off(net, i) + idx] = idx < out ? P.b[net][i][idx] : 0.f;
+          float v = 0.f;
+          if (idx < out) {
+            v = P.b[net][i][idx];
+            if constexpr (M::BAYES)
+              v = v + P.eps[ev * M::N_PARAMS + M::param_w_off(net, i) + out * in_full + idx] * fabsf(P.bs[net][i][idx]);
+          }
+          pack[M::b_off(net, i) + idx] = v;
         }
       }
     });
-    if constexpr (M::S > 0 && M::has(net, 0)) {
+    if constexpr (M::HOIST && M::has(net, 0)) {
       if (seg == 30 + net && idx < M::wsf_size(net)) {
         constexpr int KQ = M::S16 / 4, NQ = M::S16 / 16;
         constexpr int out = M::out_dim(net, 0);
@@ -1166,7 +1279,7 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
       }
     }
   });
-  if constexpr (M::S > 0) {
+  if constexpr (M::HOIST) {
     if (seg == 32 && idx < M::W0SP_SIZE) {
       // plain [merged layer-0 row][static feature] copy (dy0 static kernel)
       int om = idx / M::S16;
@@ -1228,10 +1341,8 @@ __device__ __forceinline__ int slab_to_param(int off) {
         const int f = (T - t0) * 16 + fc;
         const int o = M::frt(i, k) * 16 + row;
         constexpr int in_full = i == 0 ? M::R * M::L : M::in_dim(net, i);
-        if (o < M::out_dim(net, i) && f < M::in_dim(net, i)) {
-          const int col = i == 0 ? (f / 3) * M::L + (f % 3) : f;
-          e = M::param_w_off(net, i) + o * in_full + col;
-        }
+        const int col = i == 0 ? M::col0(f) : (f < M::in_dim(net, i) ? f : -1);
+        if (o < M::out_dim(net, i) && col >= 0) e = M::param_w_off(net, i) + o * in_full + col;
       }
     });
   });
@@ -1252,7 +1363,7 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
     const int per = (ngrid + 3) / 4, g0 = grp * per, g1 = min(ngrid, g0 + per);
     const float* p = slab + off;
 #pragma unroll 8
-    for (int gi = g0; gi < g1; ++gi) v += p[(size_t)gi * M::SLAB_TOTAL];
+    for (int gi = g0; gi < g1; ++gi) v += p[(size_t)gi * M::SLAB_STRIDE];
   }
   part[grp][lo] = v;
   __syncthreads();
@@ -1260,6 +1371,19 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
     const int e = slab_to_param<M>(off);
     if (e >= 0) dparams[e] = (part[0][lo] + part[1][lo]) + (part[2][lo] + part[3][lo]);
   }
+}
+
+// BAYES: the eps stream ([eval][N_PARAMS], torch order) re-laid out per evaluation in
+// slab order (dW tiles in MFMA C order, bias rows), the layout the backward weights
+// each evaluation's dW / bias sums with.  Padding slots get 0.
+template <class M>
+__global__ __launch_bounds__(256) void ude_eps_slab_kernel(const float* __restrict__ eps,
+                                                           float* __restrict__ eslab) {
+  const int off = blockIdx.x * 256 + threadIdx.x;
+  const size_t ev = blockIdx.y;
+  if (off >= M::SLAB_TOTAL) return;
+  const int p = slab_to_param<M>(off);
+  eslab[ev * M::SLAB_TOTAL + off] = p >= 0 ? eps[ev * M::N_PARAMS + p] : 0.f;
 }
 
 // ============================================================================

@@ -1,13 +1,14 @@
-// Compile-time description of one UDE right-hand side (lib/models.py Fp / Fa / FaFp)
-// and every derived layout the gfx950 kernels use.  All of it is constexpr so
-// that per-wave register tiles (dW accumulators, static-hoist tiles) are
-// indexed with compile-time constants and never spill to scratch.
+// Compile-time description of one UDE right-hand side (lib/models.py Fp / Fa / FaFp,
+// lib/in_development/models_bayes.py Bayes_Fp / Bayes_Fa / Bayes_FaFp) and every
+// derived layout the gfx950 kernels use.  All of it is constexpr so that per-wave
+// register tiles (dW accumulators, static-hoist tiles) are indexed with compile-time
+// constants and never spill to scratch.
 //
-// Reference layer rule (lib/models.py:118-124, :208-223): for hidden sizes
-// [h1..hk] the Linears are in->h1, h1->h2, ..., hk->out with an ELU after
-// Linear i only for i < k-1 (the last hidden Linear and the output Linear
-// have no activation).  P-net ("net"/"Fp_net") outputs 2R rates, A-net
-// ("aug_net") outputs 3R augmentation fluxes.
+// Reference layer rule (lib/models.py:118-124, :208-223, models_bayes.py:78-84): for
+// hidden sizes [h1..hk] the Linears are in->h1, h1->h2, ..., hk->out with an ELU after
+// Linear i only for i < k-1 (the last hidden Linear and the output Linear have no
+// activation).  P-net ("net"/"Fp_net") outputs 2R rates, A-net ("aug_net") outputs 3R
+// augmentation fluxes.
 #pragma once
 
 namespace ude {
@@ -20,7 +21,9 @@ constexpr int pad16(int x) { return (x + 15) & ~15; }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
-enum : int { KIND_FP = 1, KIND_FA = 2, KIND_FAFP = 3 };
+// KIND bit 4: Bayesian RHS (models_bayes.py Dense_Variational, :43-48): every
+// evaluation uses its own weight sample w_e = mu + eps_e * |std|.
+enum : int { KIND_FP = 1, KIND_FA = 2, KIND_FAFP = 3, KIND_BAYES = 4 };
 
 template <int R_, int L_, int KIND_, int NPH_, int P0_, int P1_, int P2_, int P3_,
           int NAH_, int A0_, int A1_, int A2_, int A3_>
@@ -28,11 +31,17 @@ struct Model {
   static constexpr int R = R_, L = L_, KIND = KIND_;
   static constexpr bool HAS_P = (KIND & 1) != 0;
   static constexpr bool HAS_A = (KIND & 2) != 0;
+  static constexpr bool BAYES = (KIND & KIND_BAYES) != 0;
   static constexpr int NPH = NPH_, NAH = NAH_;
   static constexpr int F = 3 * R;            // dynamic features: S, I, R of every region
   static constexpr int S = R * (L - 3);      // static features: latent dims >= 3 (zero derivative)
   static constexpr int F16 = pad16(F);
   static constexpr int S16 = pad16(S);
+  // Deterministic weights: the static features' layer-0 contribution is a per-tile
+  // constant (hoisted).  Bayesian weights change every evaluation, so layer 0 reads
+  // [dynamic | static] features as one K = F16 + S16 input instead (FULL0).
+  static constexpr bool HOIST = S > 0 && !BAYES;
+  static constexpr bool FULL0 = S > 0 && BAYES;
 
   static constexpr int nl(int net) { return net == 0 ? (HAS_P ? NPH + 1 : 0) : (HAS_A ? NAH + 1 : 0); }
   static constexpr int D = cmax(nl(0), nl(1));
@@ -42,7 +51,14 @@ struct Model {
                     : (i == 0 ? A0_ : i == 1 ? A1_ : i == 2 ? A2_ : A3_);
   }
   static constexpr bool has(int net, int i) { return i >= 0 && i < nl(net); }
-  static constexpr int in_dim(int net, int i) { return i == 0 ? F : hid(net, i - 1); }
+  // layer-0 input width in the record: F dynamic features (FULL0: + the static ones
+  // from F16 on, see col0)
+  static constexpr int in_dim(int net, int i) { return i == 0 ? (FULL0 ? F16 + S : F) : hid(net, i - 1); }
+  // layer-0 record feature f -> torch column of the flattened (R, L) state, -1 = padding
+  static constexpr int col0(int f) {
+    return f < F ? (f / 3) * L + (f % 3)
+                 : (FULL0 && f >= F16 && f < F16 + S) ? ((f - F16) / (L - 3)) * L + 3 + (f - F16) % (L - 3) : -1;
+  }
   static constexpr int out_dim(int net, int i) { return i < nh(net) ? hid(net, i) : (net == 0 ? 2 * R : 3 * R); }
   static constexpr bool act(int net, int i) { return i < nh(net) - 1; }
   static constexpr int kin(int net, int i) { return pad16(in_dim(net, i)); }
@@ -60,9 +76,9 @@ struct Model {
   static constexpr int fowner(int d, int k) { return (FTbase(d) + k) % WAVES; }
 
   // ---- input-gradient (dX) row tiles at depth d --------------------------------
-  // d > 0: rows are the inputs of layer d of each net; d == 0: the dynamic features
-  // (both nets' layer-0 contributions summed in one accumulator).
-  static constexpr int XT(int d) { return d == 0 ? F16 / 16 : rti(0, d) + rti(1, d); }
+  // d > 0: rows are the inputs of layer d of each net; d == 0: the layer-0 input
+  // features (both nets' layer-0 contributions summed in one accumulator).
+  static constexpr int XT(int d) { return d == 0 ? (FULL0 ? F16 + S16 : F16) / 16 : rti(0, d) + rti(1, d); }
   static constexpr int xnet(int d, int m) { return m < rti(0, d) ? 0 : 1; }
   static constexpr int xrt(int d, int m) { return m < rti(0, d) ? m : m - rti(0, d); }
   static constexpr int xowner(int d, int m) {
@@ -72,8 +88,10 @@ struct Model {
 
   // ---- LDS record: one row of SR floats per trajectory ([t][feature]) ---------
   static constexpr int Y_OFF = 0;
+  // FULL0: the static features sit right after the dynamic ones for the whole tile
+  static constexpr int ACT0 = FULL0 ? F16 + S16 : F16;
   static constexpr int act_off(int net, int i) {
-    int o = F16;
+    int o = ACT0;
     for (int n = 0; n < 2; ++n)
       for (int j = 0; j < nl(n); ++j) {
         if (n == net && j == i) return o;
@@ -82,11 +100,11 @@ struct Model {
     return o;
   }
   static constexpr int ACT_END = act_off(2, 0);
-  // tile-level aliases over the activation region (only live outside the step loop)
-  static constexpr int G0_OFF = F16;                // backward: merged layer-0 gradient sums
-  static constexpr int XSB_OFF = F16 + K0;          // backward: static features
-  static constexpr int XSF_OFF = F16;               // forward: static features
-  static constexpr int ALIAS_END = cmax(ACT_END, F16 + K0 + S16);
+  // static features in the record (HOIST: aliases the activation region, only live
+  // outside the step loop; FULL0: persistent, right after the dynamic features)
+  static constexpr int XSB_OFF = FULL0 ? F16 : F16 + K0;   // backward
+  static constexpr int XSF_OFF = F16;                      // forward
+  static constexpr int ALIAS_END = FULL0 ? ACT_END : cmax(ACT_END, F16 + K0 + S16);
   static constexpr int gbs(int net) {
     int m = 0;
     for (int j = 0; j < nl(net); ++j) m = cmax(m, kout(net, j));
@@ -107,8 +125,10 @@ struct Model {
   static constexpr int RK_DK1 = RK_ACCY + F4;
   static constexpr int RK_DK2 = RK_DK1 + F4;
   static constexpr int RK_DK3 = RK_DK2 + F4;
+  // FULL0 backward: per-trajectory static-feature input gradients summed over the solve
+  static constexpr int DYS_OFF = RK_DK3 + F4;
   static constexpr int REC_F = cmax(ACT_END, F16 + S16);
-  static constexpr int REC_B = RK_DK3 + F4;
+  static constexpr int REC_B = DYS_OFF + (FULL0 ? S16 : 0);
   // row stride == 4 (mod 64) floats: conflict-free b128 fragment reads, and rows
   // t and t+4 land 16 banks apart for the dW b32 reads.
   static constexpr int stride(int n) { return ((n + 59) / 64) * 64 + 4; }
@@ -117,9 +137,12 @@ struct Model {
   static constexpr int LDS_F = TT * SR_F * 4;
   // + per-workgroup bias-gradient row sums (one float per forward row tile row)
   static constexpr int DB_LDS = TT * SR_B;
+  static constexpr int NDB = 16 * FTbase_total();
+  // BAYES: + the eps-weighted bias row sums (gradient of |b_std|)
+  static constexpr int DBS_LDS = DB_LDS + NDB;
   // + staging slot for the next stage's checkpointed input ([t][F4], prefetched
   // during the flux pass)
-  static constexpr int STG_LDS = DB_LDS + 16 * FTbase_total();
+  static constexpr int STG_LDS = DB_LDS + (BAYES ? 2 : 1) * NDB;
   static constexpr int LDS_B = (STG_LDS + TT * F4) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");
 
@@ -129,6 +152,7 @@ struct Model {
   //  B(net,i):  [kout]                       bias, zero padded
   //  WSF(net):  [rto(net,0)][S16/16][64][4]  layer-0 static columns (per-tile hoist)
   //  W0SP:      [K0][S16]                    layer-0 static columns, plain, merged nets (dy0 static)
+  // BAYES: one such pack per RHS evaluation (PACK_TOTAL floats apart), no WSF / W0SP.
   static constexpr int wf_size(int net, int i) { return has(net, i) ? rto(net, i) * (kin(net, i) / 16) * 256 : 0; }
   static constexpr int wt_size(int net, int i) { return has(net, i) ? rti(net, i) * (kout(net, i) / 16) * 256 : 0; }
   static constexpr int b_size(int net, int i) { return has(net, i) ? kout(net, i) : 0; }
@@ -146,10 +170,10 @@ struct Model {
   static constexpr int wt_off(int net, int i) { return layer_pack_off(net, i) + wf_size(net, i); }
   static constexpr int b_off(int net, int i) { return wt_off(net, i) + wt_size(net, i); }
   static constexpr int LAYERS_END = layer_pack_off(2, 0);
-  static constexpr int wsf_size(int net) { return (S > 0 && has(net, 0)) ? rto(net, 0) * (S16 / 16) * 256 : 0; }
+  static constexpr int wsf_size(int net) { return (HOIST && has(net, 0)) ? rto(net, 0) * (S16 / 16) * 256 : 0; }
   static constexpr int wsf_off(int net) { return LAYERS_END + (net == 0 ? 0 : wsf_size(0)); }
   static constexpr int W0SP_OFF = LAYERS_END + wsf_size(0) + wsf_size(1);
-  static constexpr int W0SP_SIZE = S > 0 ? K0 * S16 : 0;
+  static constexpr int W0SP_SIZE = HOIST ? K0 * S16 : 0;
   static constexpr int PACK_TOTAL = W0SP_OFF + W0SP_SIZE;
 
   // ---- per-workgroup gradient slab -------------------------------------------------
@@ -166,8 +190,11 @@ struct Model {
   static constexpr int NCS = S16 / 16;
   static constexpr int SLAB_DB = N_DYN_TILES * 256;
   static constexpr int SLAB_TOTAL = SLAB_DB + FTbase(D) * 16;
-  // static-feature gradient work (outside the main kernel): per-tile layer-0 row sums
-  // G0[tile][K0][16] and split-K partials of dW0[:, static]
+  // BAYES: each workgroup slab holds [d mean | d |std|]; the eps stream is laid out
+  // per evaluation in this same slab order (SLAB_TOTAL floats per evaluation)
+  static constexpr int SLAB_STRIDE = SLAB_TOTAL * (BAYES ? 2 : 1);
+  // static-feature gradient work (outside the main kernel, HOIST only): per-tile
+  // layer-0 row sums G0[tile][K0][16] and split-K partials of dW0[:, static]
   static constexpr int STATIC_CHUNKS = 128;
 
   // ---- per-wave register tiles -----------------------------------------------------
@@ -181,6 +208,17 @@ struct Model {
     return s;
   }
   static constexpr int NDW(int w) { return ndw_before(w, D, 0); }
+  // dW tiles wave w accumulates in phase (layer) d
+  static constexpr int ndw_phase(int w, int d) {
+    int s = 0;
+    for (int kk = 0; kk < FT(d); ++kk)
+      if (fowner(d, kk) == w) s += rti(fnet(d, kk), d);
+    return s;
+  }
+  static constexpr int max_ndw() { return cmax(cmax(NDW(0), NDW(1)), cmax(NDW(2), NDW(3))); }
+  // BAYES keeps a second (eps-weighted) accumulator per dW tile in registers; larger
+  // models are not compiled in (ude_supported() reports them as unsupported)
+  static constexpr bool FITS = !BAYES || max_ndw() <= 20;
   static constexpr int ng_before(int w, int d, int k) {
     int s = 0;
     for (int e = 0; e < D; ++e)
@@ -234,6 +272,8 @@ struct Model {
     return o;
   }
   static constexpr int N_PARAMS = param_w_off(2, 0);
+  // floats of the flat gradient output: BAYES = [d mean (torch order) | d |std|]
+  static constexpr int N_GRAD = N_PARAMS * (BAYES ? 2 : 1);
   static constexpr int PAIRS = R * TT;
   static constexpr int SLOTS = (PAIRS + NTHREADS - 1) / NTHREADS;
 };

@@ -43,6 +43,15 @@ int ude_pack_weights(const UdeModelDesc* m, const float* const* W, const float* 
   return e->pack(W, b, pack, (hipStream_t)stream);
 }
 
+int ude_pack_weights_bayes(const UdeModelDesc* m, const UdeProblem* p, const float* const* W_mean,
+                           const float* const* b_mean, const float* const* W_std, const float* const* b_std,
+                           const float* eps, float* pack, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || !W_mean || !b_mean || !W_std || !b_std || !eps || !pack) return UDE_E_INVALID;
+  return e->pack_bayes(p, W_mean, b_mean, W_std, b_std, eps, pack, (hipStream_t)stream);
+}
+
 int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
                     const float* y0, float* latent, float* ckpt, double* stats_slab, float* stats_out,
                     ude_stream_t stream) {

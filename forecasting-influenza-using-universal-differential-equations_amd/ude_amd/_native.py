@@ -35,8 +35,8 @@ UDE_OK, UDE_E_UNSUPPORTED, UDE_E_INVALID, UDE_E_HIP = 0, -1, -2, -3
 _ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "invalid argument",
          UDE_E_HIP: "HIP runtime error"}
 
-EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_rk4_forward",
-                    "ude_rk4_backward", "ude_build_info")
+EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_weights_bayes",
+                    "ude_rk4_forward", "ude_rk4_backward", "ude_build_info")
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -98,6 +98,9 @@ class NativeLib:
         L.ude_query.restype = i32
         L.ude_pack_weights.argtypes = [pdesc, ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp]
         L.ude_pack_weights.restype = i32
+        pvp = ctypes.POINTER(vp)
+        L.ude_pack_weights_bayes.argtypes = [pdesc, pprob, pvp, pvp, pvp, pvp, vp, vp, vp]
+        L.ude_pack_weights_bayes.restype = i32
         L.ude_rk4_forward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_rk4_forward.restype = i32
         L.ude_rk4_backward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -118,6 +121,14 @@ class NativeLib:
         W = (ctypes.c_void_p * n)(*w_ptrs)
         B = (ctypes.c_void_p * n)(*b_ptrs)
         check(self.lib.ude_pack_weights(ctypes.byref(desc), W, B, pack_ptr, stream), "ude_pack_weights")
+
+    def pack_bayes(self, desc, prob, w_mean: Sequence[int], b_mean: Sequence[int], w_std: Sequence[int],
+                   b_std: Sequence[int], eps_ptr: int, pack_ptr: int, stream: int) -> None:
+        n = len(w_mean)
+        arr = lambda ptrs: (ctypes.c_void_p * n)(*ptrs)
+        check(self.lib.ude_pack_weights_bayes(ctypes.byref(desc), ctypes.byref(prob), arr(w_mean), arr(b_mean),
+                                              arr(w_std), arr(b_std), eps_ptr, pack_ptr, stream),
+              "ude_pack_weights_bayes")
 
     def forward(self, desc, prob, pack, sched, y0, latent, ckpt, stats_slab, stats_out, stream) -> None:
         check(self.lib.ude_rk4_forward(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, latent, ckpt,
@@ -205,8 +216,8 @@ def prebuilt() -> NativeLib:
 
 def jit_library(cfg: _cfgs.Config) -> NativeLib:
     key = _cfgs.config_key(cfg)
-    h = hashlib.sha1(open(os.path.join(CSRC, "ude_kernels.h"), "rb").read()
-                     + open(os.path.join(CSRC, "ude_model.h"), "rb").read()).hexdigest()[:10]
+    h = hashlib.sha1(b"".join(open(os.path.join(CSRC, f), "rb").read()
+                              for f in ("ude_kernels.h", "ude_model.h", "ude_entry.h", "ude_rk4.hip"))).hexdigest()[:10]
     path = os.path.join(JIT_DIR, f"libude_rk4_{key}_{h}.so")
     if not os.path.exists(path):
         os.makedirs(JIT_DIR, exist_ok=True)
@@ -225,6 +236,25 @@ def library_for(cfg: _cfgs.Config) -> NativeLib:
     if not lib.supported(desc):
         raise UdeError(f"no gfx950 kernel for {cfg}")
     return lib
+
+
+_SUPPORTED: Dict[_cfgs.Config, bool] = {}
+
+
+def config_supported(cfg: _cfgs.Config) -> bool:
+    """Whether a fused kernel exists (prebuilt, or JIT-compiled here) for cfg.
+
+    Bayesian models keep a second dW accumulator per tile in registers; models
+    too large for that are compiled but report unsupported (Model::FITS)."""
+    hit = _SUPPORTED.get(cfg)
+    if hit is None:
+        try:
+            library_for(cfg)
+            hit = True
+        except UdeError:
+            hit = False
+        _SUPPORTED[cfg] = hit
+    return hit
 
 
 def loaded_paths() -> List[str]:

@@ -5,13 +5,20 @@ Every Linear is a ``Dense_Variational``: on EACH call a fresh weight sample
 sees new weights.  Same names, constructor signatures, ``state_dict`` keys
 (``w_mean``, ``w_std``, ``b_mean``, ``b_std``) and ``get_kl`` as the reference.
 
-These run eagerly (PyTorch ops per evaluation): the fused kernel needs the
-per-evaluation noise streams injected, which is the next row of the build plan
-(SURVEY section 8f, rank 1).
+Called directly (or by a non-fused solver) a module draws its noise with
+``torch.randn_like`` per layer per call, as the reference.  Inside
+``odeint(..., method='rk4')`` on a HIP device the whole solve runs in the fused
+gfx950 kernel instead (``fused.FusedBayesRK4``): the solve's draws are one
+``(4 * n_steps, n_params)`` standard-normal stream -- row e for RHS evaluation e,
+each row in the order the reference's layers call ``make_z`` within one
+evaluation (torch parameter order) -- from torch's generator on the device, or
+the stream set with ``set_eps_stream`` (used by the parity tests to inject the
+reference's draws).
 """
 from __future__ import annotations
 
 import math
+from typing import List, Optional, Tuple
 
 import torch
 from torch import nn
@@ -92,6 +99,40 @@ def _kl_of(stacks):
 
 class _BayesBase(_UDEModule):
     uncertainty = "bayes"
+
+    # -- description consumed by the fused solver ---------------------------------
+    def ude_config(self):
+        kind, R, L, net, aug = super().ude_config()
+        return ("B" + kind, R, L, net, aug)
+
+    def _variational(self) -> List[Dense_Variational]:
+        out: List[Dense_Variational] = []
+        if self.ode_type in ("Fp", "FaFp"):
+            out += [m for m in self.Fp_net if isinstance(m, Dense_Variational)]
+        if self.ode_type in ("Fa", "FaFp"):
+            out += [m for m in self.aug_net if isinstance(m, Dense_Variational)]
+        return out
+
+    def ude_mean_std(self) -> Tuple[List[torch.Tensor], List[torch.Tensor]]:
+        """(means, stds) in C-ABI / torch order: per layer weight then bias, rate net first."""
+        mus, sds = [], []
+        for lay in self._variational():
+            mus += [lay.w_mean, lay.b_mean]
+            sds += [lay.w_std, lay.b_std]
+        return mus, sds
+
+    def set_eps_stream(self, eps: Optional[torch.Tensor]) -> None:
+        """Use ``eps`` ((4 * n_steps, n_params)) as the draws of the next fused solve."""
+        self._eps_next = eps
+
+    def take_eps(self, n_eval: int, n_params: int, device) -> torch.Tensor:
+        eps = getattr(self, "_eps_next", None)
+        self._eps_next = None
+        if eps is None:
+            return torch.randn((n_eval, n_params), device=device)
+        if tuple(eps.shape) != (n_eval, n_params):
+            raise ValueError(f"eps stream has shape {tuple(eps.shape)}, the solve needs {(n_eval, n_params)}")
+        return eps.to(device=device, dtype=torch.float32)
 
 
 class Bayes_Fp(_BayesBase):

@@ -14,12 +14,19 @@ from typing import List, Optional, Sequence, Tuple
 
 Config = Tuple[str, int, int, Optional[Tuple[int, ...]], Optional[Tuple[int, ...]]]
 
-KIND_CODE = {"Fp": 1, "Fa": 2, "FaFp": 3}
+# "B" prefix: the Bayesian right-hand sides of lib/in_development/models_bayes.py
+# (UDE_KIND_BAYES = 4 in include/ude_rk4.h)
+KIND_CODE = {"Fp": 1, "Fa": 2, "FaFp": 3, "BFp": 5, "BFa": 6, "BFaFp": 7}
+
+
+def base_kind(kind: str) -> str:
+    return kind[1:] if kind.startswith("B") else kind
 
 
 def _c(kind: str, R: int, L: int, net: Optional[Sequence[int]], aug: Optional[Sequence[int]]) -> Config:
-    return (kind, R, L, tuple(net) if net is not None and kind != "Fa" else None,
-            tuple(aug) if aug is not None and kind != "Fp" else None)
+    b = base_kind(kind)
+    return (kind, R, L, tuple(net) if net is not None and b != "Fa" else None,
+            tuple(aug) if aug is not None and b != "Fp" else None)
 
 
 PREBUILT: List[Config] = []
@@ -34,6 +41,13 @@ PREBUILT += [
     _c("Fa", 1, 8, None, [32, 32]),
     _c("Fp", 1, 6, [24], None),                      # golden: fp_r1_onehidden
     _c("FaFp", 3, 5, [40, 24], [36], ),              # golden: fafp_r3_l5_ragged
+    # Bayesian RHS (run_ode.py:99 'CONNb' / 'UONNb' / 'SONNb'), US model sizes
+    _c("BFaFp", 1, 8, [64, 64, 32], [64, 64]),
+    _c("BFp", 1, 8, [64, 64, 32], None),
+    _c("BFa", 1, 8, None, [64, 64]),
+    _c("BFaFp", 1, 8, [20, 20], [32, 32]),           # models_bayes.py class defaults
+    _c("BFp", 1, 8, [20, 20], None),
+    _c("BFa", 1, 8, None, [32, 32]),
 ]
 
 

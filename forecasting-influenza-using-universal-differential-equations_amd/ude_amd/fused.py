@@ -108,12 +108,80 @@ class FusedRK4(torch.autograd.Function):
                           dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
-        grads = []
-        off = 0
-        for shp in plan.param_shapes:
-            n = 1
-            for s in shp:
-                n *= s
-            grads.append(dparams[off:off + n].view(shp))
-            off += n
-        return (None, dy0) + tuple(grads)
+        return (None, dy0) + tuple(_split(dparams, plan.param_shapes))
+
+
+def _split(flat: torch.Tensor, shapes) -> List[torch.Tensor]:
+    out, off = [], 0
+    for shp in shapes:
+        n = 1
+        for s in shp:
+            n *= s
+        out.append(flat[off:off + n].view(shp))
+        off += n
+    return out
+
+
+class FusedBayesRK4(torch.autograd.Function):
+    """Bayesian RHS (lib/in_development/models_bayes.py): every RHS evaluation of the
+    solve uses its own weight sample w_e = mean + eps_e * |std| (Dense_Variational
+    .forward, :43-48), eps = the (4 n_steps, n_params) draw stream.
+
+    Inputs: plan, y0, eps, then the means (w, b per layer, torch order) and the raw
+    stds in the same order.  The kernel returns d/d mean and d/d |std|; the sign of
+    std (torch's abs backward) is applied here."""
+
+    @staticmethod
+    def forward(ctx, plan: Plan, y0: torch.Tensor, eps: torch.Tensor, *params: torch.Tensor):
+        dev = y0.device
+        stream = _stream(dev)
+        sz = plan.sizes
+        k = len(params) // 2
+        mus = [p.contiguous() for p in params[:k]]
+        sds = [p.contiguous() for p in params[k:]]
+        eps = eps.contiguous()
+        pack = torch.empty(max(sz.pack_bytes // 4, 1), dtype=torch.float32, device=dev)
+        plan.lib.pack_bayes(plan.desc, plan.prob, [w.data_ptr() for w in mus[0::2]], [b.data_ptr() for b in mus[1::2]],
+                            [w.data_ptr() for w in sds[0::2]], [b.data_ptr() for b in sds[1::2]], eps.data_ptr(),
+                            pack.data_ptr(), stream)
+        latent = torch.empty((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
+        need_grad = any(ctx.needs_input_grad[1:])
+        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) if need_grad else None
+        stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
+        stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
+        plan.lib.forward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                         latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), stats.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
+        ctx.plan = plan
+        if need_grad:
+            ctx.save_for_backward(y0, pack, ckpt, stats, *sds)
+        return latent, stats
+
+    @staticmethod
+    def backward(ctx, dlatent, dstats):
+        plan: Plan = ctx.plan
+        y0, pack, ckpt, stats, *sds = ctx.saved_tensors
+        dev = y0.device
+        stream = _stream(dev)
+        if dlatent is None:
+            dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
+        dlatent = dlatent.contiguous().to(torch.float32)
+        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+        dy0 = torch.empty_like(y0)
+        slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
+        plan.lib.backward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                          _ptr(ckpt), dlatent.data_ptr(), stats.data_ptr(), dstats.data_ptr(),
+                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
+        n = plan.sizes.n_params // 2
+        d_mu = _split(dparams[:n], plan.param_shapes)
+        d_abs = _split(dparams[n:], plan.param_shapes)
+        d_sd = [g * torch.sign(s) for g, s in zip(d_abs, sds)]
+        return (None, dy0, None) + tuple(d_mu) + tuple(d_sd)

@@ -6,9 +6,10 @@ event_fn=None)`` as imported by lib/VAE.py:5 and run_ode.py:24 and called as
 (lib/VAE.py:137, tuning/tune_encoders.py:221, tuning/tune_node.py:204).
 
 Dispatch:
-* ``method='rk4'`` + an RHS of this package (Fp / Fa / FaFp) + fp32 state on a
-  HIP device  ->  the fused gfx950 kernel (forward + VJP), no fallback: a
-  missing or unloadable library raises;
+* ``method='rk4'`` + an RHS of this package (Fp / Fa / FaFp, and the
+  Bayes_* classes of lib/in_development/models_bayes.py at the sizes the
+  kernels hold) + fp32 state on a HIP device  ->  the fused gfx950 kernel
+  (forward + VJP), no fallback: a missing or unloadable library raises;
 * anything else (other callables, CPU tensors, fixed-grid 'euler' /
   'midpoint' / 'rk4')  ->  the generic step-by-step solver below, which calls
   ``func`` once per stage exactly as torchdiffeq does.  Setting
@@ -26,6 +27,7 @@ import torch
 from .rhs import _UDEModule
 from .schedule import build_schedule, fixed_grid
 from . import fused as _fused
+from . import _native
 
 FIXED_METHODS = ("rk4", "euler", "midpoint")
 ADAPTIVE_METHODS = ("dopri8", "dopri5", "bosh3", "fehlberg2", "adaptive_heun", "explicit_adams",
@@ -46,10 +48,16 @@ def _check_t(t: torch.Tensor) -> None:
 
 
 def fusable(func, y0: torch.Tensor) -> bool:
-    return (isinstance(func, _UDEModule) and func.uncertainty == "none" and y0.is_cuda
+    if not (isinstance(func, _UDEModule) and y0.is_cuda
             and y0.dtype == torch.float32 and y0.dim() == 3
             and y0.shape[1] == func.n_regions and y0.shape[2] == func.latent_dim
-            and all(p.is_cuda and p.dtype == torch.float32 for p in func.parameters()))
+            and all(p.is_cuda and p.dtype == torch.float32 for p in func.parameters())):
+        return False
+    if func.uncertainty == "bayes":
+        # the Bayesian kernels hold two dW accumulator sets in registers: the models
+        # that fit are compiled (R = 1 at the reference's sizes; see Model::FITS)
+        return _native.config_supported(func.ude_config())
+    return func.uncertainty == "none"
 
 
 # Host-side caches so that a training loop calling odeint with the same time grid
@@ -86,10 +94,14 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         step_size = step_size.detach().cpu()
     step_key = None if step_size is None else (
         step_size.to(th.dtype).numpy().tobytes() if isinstance(step_size, torch.Tensor) else float(step_size))
-    lins = func.ude_linears()
-    params = []
-    for lin in lins:
-        params += [lin.weight, lin.bias]
+    bayes = func.uncertainty == "bayes"
+    if bayes:
+        mus, sds = func.ude_mean_std()
+        params = mus + sds
+    else:
+        params = []
+        for lin in func.ude_linears():
+            params += [lin.weight, lin.bias]
     cfg = func.ude_config()
     fa_w = func.fa_weight()
     key = (cfg, str(th.dtype), th.numpy().tobytes(), step_key, int(y0.shape[0]), float(fa_w), str(y0.device),
@@ -97,11 +109,17 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
     plan = _PLAN_CACHE.get(key)
     if plan is None:
         sched = build_schedule(th, step_size)
-        plan = _fused.make_plan(cfg, sched, y0.shape[0], fa_w, y0.device, [p.shape for p in params])
+        shapes = [p.shape for p in (mus if bayes else params)]
+        plan = _fused.make_plan(cfg, sched, y0.shape[0], fa_w, y0.device, shapes)
         _lru_put(_PLAN_CACHE, key, plan)
     else:
         _PLAN_CACHE.move_to_end(key)
-    latent, stats = _fused.FusedRK4.apply(plan, y0.contiguous(), *params)
+    if bayes:
+        n_par = sum(int(p.numel()) for p in mus)
+        eps = func.take_eps(4 * plan.prob.n_steps, n_par, y0.device)
+        latent, stats = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *params)
+    else:
+        latent, stats = _fused.FusedRK4.apply(plan, y0.contiguous(), *params)
     func._record_fused(stats, plan.n_eval)
     return latent
 

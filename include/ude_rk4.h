@@ -38,7 +38,11 @@ enum {
   UDE_E_HIP = -3          /* a HIP runtime call failed                      */
 };
 
-enum { UDE_KIND_FP = 1, UDE_KIND_FA = 2, UDE_KIND_FAFP = 3 };
+/* kind: Fp / Fa / FaFp, optionally | UDE_KIND_BAYES for the Bayesian right-hand
+ * sides Bayes_Fp / Bayes_Fa / Bayes_FaFp of lib/in_development/models_bayes.py
+ * (:69-265), whose Dense_Variational layers (:12-48) draw a fresh weight sample
+ * w = w_mean + eps * |w_std| at every evaluation. */
+enum { UDE_KIND_FP = 1, UDE_KIND_FA = 2, UDE_KIND_FAFP = 3, UDE_KIND_BAYES = 4 };
 
 /* The RHS module: lib/models.py FaFp(n_regions, latent_dim, net_sizes,
  * aug_net_sizes) etc.  Hidden-size lists of up to 4 entries. */
@@ -94,6 +98,21 @@ int ude_query(const UdeModelDesc* m, const UdeProblem* p, int device, UdeSizes* 
  * W[i] / b[i]: P-net layers first (i = 0..n_p_hidden), then A-net layers. */
 int ude_pack_weights(const UdeModelDesc* m, const float* const* W, const float* const* b,
                      float* pack, ude_stream_t stream);
+
+/* Bayesian models (kind & UDE_KIND_BAYES): the per-evaluation weight samples of
+ * one solve.  Replaces Dense_Variational.make_z + forward (models_bayes.py:30-48),
+ * called 4 * n_steps times per solve by the reference: eps (device) is that draw
+ * stream, [4 * n_steps][n_params / 2] floats, row e feeding evaluation e (stage
+ * e % 4 of step e / 4), each row in torch parameter order (per layer: weight
+ * (out, in) then bias; rate net first) -- the order the reference's layers call
+ * make_z within one evaluation.  W_* / b_*: the layers' w_mean / b_mean /
+ * w_std / b_std (|std| is taken here).  pack is sized by ude_query
+ * (pack_bytes) and holds every sample plus the eps stream the backward needs.
+ * For Bayesian models ude_query's n_params is 2 x the parameter count and
+ * ude_rk4_backward's dparams = [d mean (torch order) | d |std| (torch order)]. */
+int ude_pack_weights_bayes(const UdeModelDesc* m, const UdeProblem* p, const float* const* W_mean,
+                           const float* const* b_mean, const float* const* W_std, const float* const* b_std,
+                           const float* eps, float* pack, ude_stream_t stream);
 
 /* Forward solve.  latent: (T, N, R, L) with T = n_out + 1.  If ckpt != NULL
  * the stage states are saved for ude_rk4_backward.  stats_out (device, 5

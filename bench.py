@@ -44,6 +44,10 @@ WORKLOADS = {
     "us_northstar": dict(kind="FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=4096,
                          t=("arange", 366, 7.0),
                          desc="US model R=1, 4096 trajectories x 365 daily RK4 steps (north-star M1)"),
+    "bayes_us": dict(kind="Bayes_FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=4096,
+                     t=("arange", 366, 7.0),
+                     desc="Bayesian US model (models_bayes.py Bayes_FaFp, fresh weight sample per RHS "
+                          "evaluation), R=1, 4096 trajectories x 365 daily RK4 steps"),
 }
 
 
@@ -73,7 +77,11 @@ def synthetic_y0(gen, N, R, L):
 
 def build(pkg, w, device, seed):
     torch.manual_seed(0)                         # identical weights on every rank
-    cls = getattr(pkg, w["kind"])
+    if w["kind"].startswith("Bayes_"):
+        from ude_amd import bayes
+        cls = getattr(bayes, w["kind"])
+    else:
+        cls = getattr(pkg, w["kind"])
     kw = {}
     if w["net"] is not None:
         kw["net_sizes"] = w["net"]
@@ -266,6 +274,14 @@ def main():
                                 "ms_per_step": el2 / 3 * 1e3, "fwd_ms": k2["fwd"], "bwd_ms": k2["bwd"],
                                 "target_rhs_evals_per_s": 1e7}
         del m2, y2, d2
+        w3 = WORKLOADS["bayes_us"]
+        m3, y3, t3, d3 = build(pkg, w3, dev, seed=9)
+        el3, k3 = time_steps(pkg, udist, m3, y3, t3, d3, 1, 3, 1, barrier)
+        v3 = w3["n_traj"] * (len(t3) - 1) * 3 / el3
+        res["bayes_M1"] = {"workload": "bayes_us", "description": w3["desc"], "traj_steps_per_s": v3,
+                           "rhs_evals_per_s": 4 * v3, "ms_per_step": el3 / 3 * 1e3, "fwd_ms": k3["fwd"],
+                           "bwd_ms": k3["bwd"]}
+        del m3, y3, d3
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(w, mod)
     if rank == 0:

@@ -98,11 +98,14 @@ class _UDEModule(nn.Module):
             torch.stack([])  # same error as the reference on an empty tracker
         if len(groups) == 1:
             _, m, s = groups[0]
-            return Normal(m, s)
-        n_tot = sum(g[0] for g in groups)
-        mean = sum(g[0] * g[1] for g in groups) / n_tot
-        ss = sum((g[0] - 1.0) * g[2] ** 2 + g[0] * (g[1] - mean) ** 2 for g in groups)
-        return Normal(mean, torch.sqrt(ss / (n_tot - 1.0)))
+        else:
+            n_tot = sum(g[0] for g in groups)
+            m = sum(g[0] * g[1] for g in groups) / n_tot
+            ss = sum((g[0] - 1.0) * g[2] ** 2 + g[0] * (g[1] - m) ** 2 for g in groups)
+            s = torch.sqrt(ss / (n_tot - 1.0))
+        # Normal's argument validation reads the device values back (two host syncs
+        # per training step on a HIP device); it stays on for host tensors
+        return Normal(m, s, validate_args=False if m.is_cuda else None)
 
     # -- description consumed by the fused solver -----------------------------
     def ude_config(self):

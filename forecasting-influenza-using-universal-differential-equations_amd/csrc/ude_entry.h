@@ -5,6 +5,7 @@
 #include <string.h>
 #include "ude_rk4.h"
 #include "ude_kernels.h"
+#include "ude_dopri5.h"
 
 namespace ude {
 
@@ -221,6 +222,118 @@ struct Ops {
   }
 };
 
+// ---- adaptive dopri5 solve (ude_dopri5.h) ------------------------------------
+template <class M>
+struct DopriOps {
+  struct Layout {
+    size_t ctl, part, stats, S, Cm, total;
+  };
+  static constexpr int CHUNK = 8;      // step attempts queued between host checks
+
+  static int attrs_grid(int device, int n_tiles, int* grid) {
+    static bool done = false;
+    if (!done) {
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_dopri_kernel<M, dp::MODE_F0>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_dopri_kernel<M, dp::MODE_TRIAL>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_dopri_kernel<M, dp::MODE_STEP>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+      done = true;
+    }
+    int cus = 0, occ = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_dopri_kernel<M, dp::MODE_STEP>, NTHREADS, M::LDS_F));
+    if (occ < 1) occ = 1;
+    const long mx = (long)cus * occ;
+    *grid = (int)(n_tiles < mx ? n_tiles : mx);
+    if (*grid < 1) *grid = 1;
+    return UDE_OK;
+  }
+
+  static Layout layout(int n_tiles, int grid) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    Layout L;
+    L.ctl = 0;
+    L.part = al(sizeof(DopriCtl));
+    L.stats = L.part + al((size_t)grid * 4 * 8);
+    L.S = L.stats + al((size_t)grid * 5 * 8);
+    L.Cm = L.S + al((size_t)2 * n_tiles * 2 * M::F * TT * 4);
+    L.total = L.Cm + al((size_t)n_tiles * M::F * TT * 4);
+    return L;
+  }
+
+  static int workspace(const UdeProblem* p, int device, int64_t* bytes) {
+    if (M::BAYES) return UDE_E_UNSUPPORTED;
+    if (p->n_traj < 1 || p->n_out < 0) return UDE_E_INVALID;
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int grid = 1;
+    int rc = attrs_grid(device, n_tiles, &grid);
+    if (rc) return rc;
+    *bytes = (int64_t)layout(n_tiles, grid).total;
+    return UDE_OK;
+  }
+
+  static int forward(const UdeProblem* p, const float* pack, const double* t_out, double rtol, double atol,
+                     double first_step, int max_steps, const float* y0, float* latent, void* ws, float* stats_out,
+                     UdeDopriInfo* info, hipStream_t s) {
+    if (M::BAYES) return UDE_E_UNSUPPORTED;
+    if (!pack || !t_out || !y0 || !latent || !ws || !stats_out || p->n_traj < 1 || p->n_out < 0) return UDE_E_INVALID;
+    if (max_steps < 1) max_steps = 1;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int grid = 1;
+    int rc = attrs_grid(dev, n_tiles, &grid);
+    if (rc) return rc;
+    const Layout L = layout(n_tiles, grid);
+    unsigned char* base = (unsigned char*)ws;
+    DArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.y0 = y0; a.t_out = t_out; a.latent = latent;
+    a.S = (float*)(base + L.S); a.Cm = (float*)(base + L.Cm);
+    a.part = (double*)(base + L.part); a.stats_slab = (double*)(base + L.stats);
+    a.ctl = (DopriCtl*)(base + L.ctl);
+    a.n_traj = p->n_traj; a.n_tiles = n_tiles; a.n_times = p->n_out + 1;
+    a.fa_w = p->fa_w; a.rtol32 = (float)rtol; a.atol32 = (float)atol;
+    const double count = (double)p->n_traj * M::R * M::L;
+    const dim3 g(grid), b(NTHREADS);
+    hipLaunchKernelGGL((ude_dopri_kernel<M, dp::MODE_F0>), g, b, M::LDS_F, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(ude_dopri_ctl_kernel<0>, dim3(1), dim3(64), 0, s, (int)dp::MODE_F0, (const double*)a.part, grid,
+                       a.ctl, t_out, a.n_times, count, max_steps, first_step);
+    if (!(first_step > 0.0)) {
+      hipLaunchKernelGGL((ude_dopri_kernel<M, dp::MODE_TRIAL>), g, b, M::LDS_F, s, a);
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(ude_dopri_ctl_kernel<0>, dim3(1), dim3(64), 0, s, (int)dp::MODE_TRIAL, (const double*)a.part,
+                       grid, a.ctl, t_out, a.n_times, count, max_steps, first_step);
+    HIPCHK(hipGetLastError());
+    DopriCtl h;
+    memset(&h, 0, sizeof(h));
+    for (long it = 0;; it += CHUNK) {
+      HIPCHK(hipMemcpyAsync(&h, a.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (h.done || h.err) break;
+      for (int i = 0; i < CHUNK; ++i) {
+        hipLaunchKernelGGL((ude_dopri_kernel<M, dp::MODE_STEP>), g, b, M::LDS_F, s, a);
+        hipLaunchKernelGGL(ude_dopri_ctl_kernel<0>, dim3(1), dim3(64), 0, s, (int)dp::MODE_STEP, (const double*)a.part,
+                           grid, a.ctl, t_out, a.n_times, count, max_steps, first_step);
+      }
+      HIPCHK(hipGetLastError());
+    }
+    if (info) {
+      info->n_steps = h.n_steps; info->n_accepted = h.n_accepted; info->n_evals = h.n_evals; info->status = h.err;
+    }
+    if (h.err) return UDE_E_SOLVER;
+    // the last accepted step's outputs (idempotent if a queued step kernel already wrote them)
+    hipLaunchKernelGGL((ude_dopri_kernel<M, dp::MODE_STEP>), g, b, M::LDS_F, s, a);
+    HIPCHK(hipGetLastError());
+    const double n_eval = (double)h.n_evals * (double)p->n_traj * (double)M::R;
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)a.stats_slab, grid,
+                       n_eval, stats_out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+};
+
 struct Entry {
   bool (*match)(const UdeModelDesc*);
   int (*query)(const UdeProblem*, int, UdeSizes*);
@@ -230,11 +343,15 @@ struct Entry {
   int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*, float*, hipStream_t);
   int (*backward)(const UdeProblem*, const float*, const void*, const float*, const float*, const float*,
                   const float*, const float*, float*, float*, float*, hipStream_t);
+  int (*dopri5_workspace)(const UdeProblem*, int, int64_t*);
+  int (*dopri5_forward)(const UdeProblem*, const float*, const double*, double, double, double, int, const float*,
+                        float*, void*, float*, UdeDopriInfo*, hipStream_t);
 };
 
 template <class M>
 constexpr Entry make_entry() {
-  return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward};
+  return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward,
+               &DopriOps<M>::workspace, &DopriOps<M>::forward};
 }
 
 

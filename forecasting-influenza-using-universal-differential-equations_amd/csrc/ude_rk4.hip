@@ -71,6 +71,23 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
                      (hipStream_t)stream);
 }
 
+int ude_dopri5_workspace(const UdeModelDesc* m, const UdeProblem* p, int device, int64_t* ws_bytes) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || !ws_bytes) return UDE_E_INVALID;
+  return e->dopri5_workspace(p, device, ws_bytes);
+}
+
+int ude_dopri5_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const double* t_out,
+                       double rtol, double atol, double first_step, int32_t max_steps, const float* y0,
+                       float* latent, void* ws, float* stats_out, UdeDopriInfo* info, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || !(rtol >= 0.0) || !(atol >= 0.0)) return UDE_E_INVALID;
+  return e->dopri5_forward(p, pack, t_out, rtol, atol, first_step, max_steps, y0, latent, ws, stats_out, info,
+                           (hipStream_t)stream);
+}
+
 #ifdef UDE_PROFILE
 void ude_debug_set_prof(unsigned long long* p) { ude::g_prof_buffer = p; }
 #endif

@@ -31,12 +31,13 @@ ARCH = os.environ.get("UDE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["-O3", "-std=c++20", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}"]
 
-UDE_OK, UDE_E_UNSUPPORTED, UDE_E_INVALID, UDE_E_HIP = 0, -1, -2, -3
+UDE_OK, UDE_E_UNSUPPORTED, UDE_E_INVALID, UDE_E_HIP, UDE_E_SOLVER = 0, -1, -2, -3, -4
 _ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "invalid argument",
-         UDE_E_HIP: "HIP runtime error"}
+         UDE_E_HIP: "HIP runtime error", UDE_E_SOLVER: "adaptive solve failed"}
 
 EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_weights_bayes",
-                    "ude_rk4_forward", "ude_rk4_backward", "ude_build_info")
+                    "ude_rk4_forward", "ude_rk4_backward", "ude_dopri5_workspace", "ude_dopri5_forward",
+                    "ude_build_info")
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -48,6 +49,11 @@ class UdeModelDesc(ctypes.Structure):
 class UdeProblem(ctypes.Structure):
     _fields_ = [("n_traj", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("n_out", ctypes.c_int32),
                 ("fa_w", ctypes.c_float)]
+
+
+class UdeDopriInfo(ctypes.Structure):
+    _fields_ = [("n_steps", ctypes.c_int32), ("n_accepted", ctypes.c_int32), ("n_evals", ctypes.c_int32),
+                ("status", ctypes.c_int32)]
 
 
 class UdeSizes(ctypes.Structure):
@@ -105,6 +111,12 @@ class NativeLib:
         L.ude_rk4_forward.restype = i32
         L.ude_rk4_backward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_rk4_backward.restype = i32
+        L.ude_dopri5_workspace.argtypes = [pdesc, pprob, i32, ctypes.POINTER(ctypes.c_int64)]
+        L.ude_dopri5_workspace.restype = i32
+        dbl = ctypes.c_double
+        L.ude_dopri5_forward.argtypes = [pdesc, pprob, vp, vp, dbl, dbl, dbl, ctypes.c_int32, vp, vp, vp, vp,
+                                         ctypes.POINTER(UdeDopriInfo), vp]
+        L.ude_dopri5_forward.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -138,6 +150,25 @@ class NativeLib:
                  stream) -> None:
         check(self.lib.ude_rk4_backward(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
                                         stats_out, dstats, dy0, slab, dparams, stream), "ude_rk4_backward")
+
+    def dopri5_workspace(self, desc, prob, device: int) -> int:
+        out = ctypes.c_int64(0)
+        check(self.lib.ude_dopri5_workspace(ctypes.byref(desc), ctypes.byref(prob), int(device), ctypes.byref(out)),
+              "ude_dopri5_workspace")
+        return int(out.value)
+
+    def dopri5_forward(self, desc, prob, pack, t_out, rtol, atol, first_step, max_steps, y0, latent, ws,
+                       stats_out, stream) -> UdeDopriInfo:
+        info = UdeDopriInfo()
+        rc = self.lib.ude_dopri5_forward(ctypes.byref(desc), ctypes.byref(prob), pack, t_out, float(rtol),
+                                         float(atol), float(first_step), int(max_steps), y0, latent, ws, stats_out,
+                                         ctypes.byref(info), stream)
+        if rc == UDE_E_SOLVER:
+            why = {1: "underflow in dt", 2: "max_num_steps exceeded", 3: "non-finite values in state `y`"}
+            raise AssertionError(f"dopri5: {why.get(info.status, info.status)} "
+                                 f"(after {info.n_steps} steps, {info.n_evals} evaluations)")
+        check(rc, "ude_dopri5_forward")
+        return info
 
     def build_info(self) -> str:
         return self.lib.ude_build_info().decode()

@@ -1,0 +1,167 @@
+"""Adaptive Dormand-Prince solves (``odeint(..., method='dopri5')``, torchdiffeq's default).
+
+Two executions of the same torchdiffeq 0.2.x algorithm (``RKAdaptiveStepsizeODESolver``
+with the Dormand-Prince-Shampine tableau, ``_select_initial_step``,
+``_optimal_step_size``, dense output by ``_interp_fit`` / ``_interp_evaluate``; one
+step size for the whole batch from the RMS error norm over every state element):
+
+* ``fused_dopri5``: the UDE right-hand sides on a HIP device without autograd
+  (validation / forecasting, ``VAE.__call__(training=False)``, lib/VAE.py:127):
+  the gfx950 kernels of csrc/ude_dopri5.h through ``ude_dopri5_forward``.  The
+  side statistics (``posterior()``, ``tracker``) cover every evaluation, rejected
+  steps and the two start-up evaluations included, as the reference's lists do.
+* ``eager_dopri5``: any callable, any device, differentiable (autograd through
+  every stage and through the step-size controller, as torchdiffeq's odeint).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from . import _native
+from . import fused as _fused
+
+_BETA = [
+    [1 / 5],
+    [3 / 40, 9 / 40],
+    [44 / 45, -56 / 15, 32 / 9],
+    [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+    [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656],
+    [35 / 384, 0.0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84],
+]
+_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1.0, 1.0]
+_C_ERROR = [35 / 384 - 1951 / 21600, 0.0, 500 / 1113 - 22642 / 50085, 125 / 192 - 451 / 720,
+            -2187 / 6784 - -12231 / 42400, 11 / 84 - 649 / 6300, -1.0 / 60.0]
+_C_MID = [6025192743 / 30085553152 / 2, 0.0, 51252292925 / 65400821598 / 2, -2691868925 / 45128329728 / 2,
+          187940372067 / 1594534317056 / 2, -1776094331 / 19743644256 / 2, 11237099 / 235043384 / 2]
+MAX_NUM_STEPS = 2 ** 31 - 1
+
+
+# ---------------------------------------------------------------------------
+# fused (HIP) forward
+# ---------------------------------------------------------------------------
+def fused_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,
+                 max_num_steps: int = MAX_NUM_STEPS) -> torch.Tensor:
+    cfg = func.ude_config()
+    lib = _native.library_for(cfg)
+    desc = _native.make_desc(cfg)
+    dev = y0.device
+    prob = _native.UdeProblem()
+    prob.n_traj = int(y0.shape[0])
+    prob.n_steps = 0
+    prob.n_out = int(len(t)) - 1
+    prob.fa_w = float(func.fa_weight())
+    dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+    sizes = lib.query(desc, prob, dev_index)
+    stream = _fused._stream(dev)
+    ws_bytes = lib.dopri5_workspace(desc, prob, dev_index)
+    pack = torch.empty(sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
+    lins = func.ude_linears()
+    ws_t = [l.weight.detach().contiguous() for l in lins]
+    bs_t = [l.bias.detach().contiguous() for l in lins]
+    lib.pack(desc, [w.data_ptr() for w in ws_t], [b.data_ptr() for b in bs_t], pack.data_ptr(), stream)
+    t64 = t.detach().to(device=dev, dtype=torch.float64).contiguous()
+    y = y0.detach().contiguous()
+    latent = torch.empty((len(t),) + tuple(y.shape), dtype=torch.float32, device=dev)
+    ws = torch.empty(max(ws_bytes // 8, 1), dtype=torch.float64, device=dev)
+    stats = torch.zeros(5, dtype=torch.float32, device=dev)
+    fs = 0.0 if first_step is None else float(first_step)
+    info = lib.dopri5_forward(desc, prob, pack.data_ptr(), t64.data_ptr(), float(rtol), float(atol), fs,
+                              min(int(max_num_steps), MAX_NUM_STEPS), y.data_ptr(), latent.data_ptr(),
+                              ws.data_ptr(), stats.data_ptr(), stream)
+    func._record_fused(stats, info.n_evals * prob.n_traj * func.n_regions)
+    func.last_solve_info = {"method": "dopri5", "n_steps": info.n_steps, "n_accepted": info.n_accepted,
+                            "n_evals": info.n_evals}
+    return latent
+
+
+# ---------------------------------------------------------------------------
+# eager (any callable, differentiable)
+# ---------------------------------------------------------------------------
+def _rms(x: torch.Tensor) -> torch.Tensor:
+    return x.abs().pow(2).mean().sqrt()
+
+
+def _dot(ks: List[torch.Tensor], c: torch.Tensor) -> torch.Tensor:
+    return torch.stack(ks, -1).matmul(c)
+
+
+def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,
+                 max_num_steps: int = MAX_NUM_STEPS) -> torch.Tensor:
+    ydt = y0.dtype
+    dev = y0.device
+    tt = t.to(device=dev, dtype=torch.float64)
+    rt = torch.as_tensor(rtol, dtype=torch.float64, device=dev)
+    at = torch.as_tensor(atol, dtype=torch.float64, device=dev)
+    beta = [torch.tensor(b, dtype=ydt, device=dev) for b in _BETA]
+    c_err = torch.tensor(_C_ERROR, dtype=ydt, device=dev)
+    c_mid = torch.tensor(_C_MID, dtype=ydt, device=dev)
+
+    t0 = tt[0]
+    f0 = func(t0.to(ydt), y0)
+    if first_step is None:
+        scale = at + torch.abs(y0) * rt
+        d0 = _rms(y0 / scale).abs()
+        d1 = _rms(f0 / scale).abs()
+        h0 = torch.tensor(1e-6, dtype=ydt, device=dev) if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+        h0 = h0.abs()
+        f1 = func(t0.to(ydt) + h0, y0 + h0 * f0)
+        d2 = torch.abs(_rms((f1 - f0) / scale) / h0)
+        if d1 <= 1e-15 and d2 <= 1e-15:
+            h1 = torch.max(torch.tensor(1e-6, dtype=ydt, device=dev), h0 * 1e-3)
+        else:
+            h1 = (0.01 / torch.max(d1, d2)) ** (1.0 / 5.0)
+        dt = torch.min(100 * h0, h1.abs()).to(torch.float64)
+    else:
+        dt = torch.as_tensor(first_step, dtype=torch.float64, device=dev)
+
+    out = [y0]
+    y, fy = y0, f0
+    t_end = t0
+    seg_t0 = t0
+    coef = None
+    n_steps = 0
+    for i in range(1, len(tt)):
+        next_t = tt[i]
+        while next_t > t_end:
+            if n_steps >= max_num_steps:
+                raise AssertionError("max_num_steps exceeded")
+            if not bool(t_end + dt > t_end):
+                raise AssertionError(f"underflow in dt {float(dt)}")
+            if not bool(torch.isfinite(y).all()):
+                raise AssertionError("non-finite values in state `y`")
+            ts, te = t_end, t_end + dt
+            dts = dt.to(ydt)
+            ks = [fy]
+            yi = y
+            for s in range(6):
+                yi = y + _dot(ks, beta[s] * dts)
+                ti = te if _ALPHA[s] == 1.0 else ts + _ALPHA[s] * dt
+                ks.append(func(ti.to(ydt), yi))
+            y1, f1 = yi, ks[-1]
+            err = _dot(ks, dts * c_err)
+            ratio = _rms(err / (at + rt * torch.max(y.abs(), y1.abs()))).abs()
+            n_steps += 1
+            if bool(ratio <= 1):
+                y_mid = y + _dot(ks, dts * c_mid)
+                a = 2 * dts * (f1 - fy) - 8 * (y1 + y) + 16 * y_mid
+                b = dts * (5 * fy - 3 * f1) + 18 * y + 14 * y1 - 32 * y_mid
+                c = dts * (f1 - 4 * fy) - 11 * y - 5 * y1 + 16 * y_mid
+                coef = [y, dts * fy, c, b, a]
+                seg_t0, t_end = ts, te
+                y, fy = y1, f1
+            if ratio == 0:
+                dt = dt * 10.0
+            else:
+                dfac = 1.0 if ratio < 1 else 0.2
+                fac = torch.clamp(0.9 / ratio.to(torch.float64) ** 0.2, min=dfac, max=10.0)
+                dt = dt * fac
+        x = ((next_t - seg_t0) / (t_end - seg_t0)).to(ydt)
+        total = coef[0] + x * coef[1]
+        xp = x
+        for cc in coef[2:]:
+            xp = xp * x
+            total = total + xp * cc
+        out.append(total)
+    return torch.stack(out, 0)

@@ -14,7 +14,10 @@ Dispatch:
   'midpoint' / 'rk4')  ->  the generic step-by-step solver below, which calls
   ``func`` once per stage exactly as torchdiffeq does.  Setting
   ``UDE_STRICT=1`` makes a UDE module that would take this path raise instead.
-Adaptive methods (dopri5, ...) are recognised but not implemented yet.
+``method='dopri5'`` (torchdiffeq's default): the fused gfx950 adaptive solve for
+a UDE module without autograd (ude_amd/adaptive.py, csrc/ude_dopri5.h), else the
+eager differentiable restatement.  Other adaptive methods raise
+NotImplementedError.
 """
 from __future__ import annotations
 
@@ -28,6 +31,7 @@ from .rhs import _UDEModule
 from .schedule import build_schedule, fixed_grid
 from . import fused as _fused
 from . import _native
+from . import adaptive as _adaptive
 
 FIXED_METHODS = ("rk4", "euler", "midpoint")
 ADAPTIVE_METHODS = ("dopri8", "dopri5", "bosh3", "fehlberg2", "adaptive_heun", "explicit_adams",
@@ -45,6 +49,10 @@ def _check_t(t: torch.Tensor) -> None:
         raise TypeError("t must be a floating point Tensor")
     if len(t) > 1 and not bool((t[1:] > t[:-1]).all()):
         raise AssertionError("t must be strictly increasing")
+
+
+def _needs_grad(func, y0: torch.Tensor) -> bool:
+    return torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in func.parameters()))
 
 
 def fusable(func, y0: torch.Tensor) -> bool:
@@ -180,8 +188,17 @@ def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, even
         _check_t(t)
     options = dict(options or {})
     step_size = options.pop("step_size", None)
+    if method == "dopri5":
+        first_step = options.pop("first_step", None)
+        max_num_steps = options.pop("max_num_steps", _adaptive.MAX_NUM_STEPS)
+        if fusable(func, y0) and func.uncertainty == "none" and not _needs_grad(func, y0):
+            return _adaptive.fused_dopri5(func, y0, t, rtol, atol, first_step, max_num_steps)
+        if isinstance(func, _UDEModule) and os.environ.get("UDE_STRICT", "0") == "1":
+            raise RuntimeError("UDE_STRICT=1: this dopri5 solve would not run on the fused gfx950 kernel "
+                               f"(grad={_needs_grad(func, y0)}, device={y0.device}, dtype={y0.dtype})")
+        return _adaptive.eager_dopri5(func, y0, t, rtol, atol, first_step, max_num_steps)
     if method in ADAPTIVE_METHODS:
-        raise NotImplementedError(f"method '{method}' is not implemented yet (fixed-grid rk4/euler/midpoint are)")
+        raise NotImplementedError(f"method '{method}' is not implemented (rk4 / euler / midpoint / dopri5 are)")
     if method == "rk4" and fusable(func, y0):
         return fused_odeint(func, y0, t, step_size)
     if isinstance(func, _UDEModule) and os.environ.get("UDE_STRICT", "0") == "1":

@@ -35,7 +35,8 @@ enum {
   UDE_OK = 0,
   UDE_E_UNSUPPORTED = -1, /* no compiled kernel for this model description */
   UDE_E_INVALID = -2,     /* bad argument (sizes, null pointers)            */
-  UDE_E_HIP = -3          /* a HIP runtime call failed                      */
+  UDE_E_HIP = -3,         /* a HIP runtime call failed                      */
+  UDE_E_SOLVER = -4       /* adaptive solve failed (see UdeDopriInfo.status) */
 };
 
 /* kind: Fp / Fa / FaFp, optionally | UDE_KIND_BAYES for the Bayesian right-hand
@@ -131,6 +132,33 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
                      const void* sched, const float* y0, const float* ckpt,
                      const float* dlatent, const float* stats_out, const float* dstats,
                      float* dy0, float* grad_slab, float* dparams, ude_stream_t stream);
+
+/* ---- adaptive Dormand-Prince solve (forward) ---------------------------------
+ * Replaces torchdiffeq.odeint(func, y0, t, rtol, atol, method='dopri5',
+ * options={'first_step': h?}) -- the default method of the solver API the
+ * reference imports (lib/VAE.py:5, run_ode.py:24) -- for the UDE right-hand
+ * sides (deterministic kinds only).  torchdiffeq semantics: one step size for
+ * the whole batch from the RMS error norm over all N*R*L state elements, accept
+ * iff error_ratio <= 1, torchdiffeq's initial-step heuristic, dense output (DPS
+ * interpolant of the last accepted step) at every t_out, float64 time
+ * arithmetic.  Stats are taken over every RHS evaluation (rejected steps and the
+ * start-up evaluations included), as the reference's params / tracker lists.
+ *   p->n_out = T - 1 (p->n_steps is ignored); t_out: T increasing float64 times
+ *   (device); latent: (T, N, R, L); ws: ude_dopri5_workspace() bytes; info
+ *   (host, may be NULL): step / evaluation counts and the failure reason
+ *   (status 1: dt underflow, 2: max_steps reached, 3: non-finite state).
+ * first_step <= 0 selects the initial step automatically.  This call waits for
+ * the device (the number of steps is data dependent): it checks the device's
+ * "done" flag every 8 step attempts. */
+typedef struct UdeDopriInfo {
+  int32_t n_steps, n_accepted, n_evals, status;
+} UdeDopriInfo;
+
+int ude_dopri5_workspace(const UdeModelDesc* m, const UdeProblem* p, int device, int64_t* ws_bytes);
+
+int ude_dopri5_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const double* t_out,
+                       double rtol, double atol, double first_step, int32_t max_steps, const float* y0,
+                       float* latent, void* ws, float* stats_out, UdeDopriInfo* info, ude_stream_t stream);
 
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);

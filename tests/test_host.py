@@ -98,7 +98,7 @@ def test_odeint_argument_checks(pkg):
     with pytest.raises(AssertionError):
         pkg.odeint(mod, y0, torch.tensor([0.0, 2.0, 1.0]), method="rk4")
     with pytest.raises(NotImplementedError):
-        pkg.odeint(mod, y0, torch.arange(3.0))           # default dopri5: not implemented yet
+        pkg.odeint(mod, y0, torch.arange(3.0), method="bosh3")
 
 
 def test_cpu_tensors_do_not_take_the_fused_path(pkg):

@@ -177,6 +177,30 @@ def cpu_baseline(w, mod_gpu, budget_s=12.0):
             "host_cpus": os.cpu_count()}
 
 
+def dopri5_line(pkg, w, dev, reps=3):
+    """BASELINE configs[2] forward: the same batch solved by the fused adaptive dopri5
+    (torchdiffeq defaults rtol 1e-7, atol 1e-9; evaluation path, no autograd)."""
+    mod, y0, t, _ = build(pkg, w, dev, seed=77)
+    y0 = y0.detach()
+    td = t.to(dev)
+    with torch.no_grad():
+        mod.clear_tracking()
+        pkg.odeint(mod, y0, td, method="dopri5")                 # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            mod.clear_tracking()
+            pkg.odeint(mod, y0, td, method="dopri5")
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / reps
+    info = mod.last_solve_info
+    evals = info["n_evals"] * w["n_traj"]
+    return {"workload": "state49 batch, method='dopri5' (rtol 1e-7, atol 1e-9), forward only",
+            "ms_per_solve": el * 1e3, "n_steps": info["n_steps"], "n_accepted": info["n_accepted"],
+            "n_evals": info["n_evals"], "rhs_evals_per_s": evals / el,
+            "traj_accepted_steps_per_s": info["n_accepted"] * w["n_traj"] / el}
+
+
 def _cpu_copy(mod):
     import copy
     mod.clear_tracking()
@@ -282,6 +306,8 @@ def main():
                            "rhs_evals_per_s": 4 * v3, "ms_per_step": el3 / 3 * 1e3, "fwd_ms": k3["fwd"],
                            "bwd_ms": k3["bwd"]}
         del m3, y3, d3
+    if rank == 0 and world == 1 and not args.no_extra and args.workload == "state49":
+        res["dopri5_state49"] = dopri5_line(pkg, w, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(w, mod)
     if rank == 0:

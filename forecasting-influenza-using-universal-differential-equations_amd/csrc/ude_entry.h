@@ -6,6 +6,7 @@
 #include "ude_rk4.h"
 #include "ude_kernels.h"
 #include "ude_dopri5.h"
+#include "ude_loss.h"
 
 namespace ude {
 
@@ -214,7 +215,7 @@ struct Ops {
       hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
                          (const float*)part, dparams);
       HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3(n_tiles), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3(n_tiles), dim3(256), TT * M::R * M::L * 4, s,
                          (const float*)g0buf, pack, dlatent, p->n_traj, p->n_out + 1, dy0);
       HIPCHK(hipGetLastError());
     }
@@ -334,6 +335,91 @@ struct DopriOps {
   }
 };
 
+// ---- fused loss head (ude_loss.h): decoder + nll_loss + latent_init_loss ----------
+template <class M>
+struct LossOps {
+  using D = LossDims<M::R>;
+  struct Layout {
+    size_t musd, part, slab, total;
+  };
+  static int grid(int device, int T, int S, int B, int* g) {
+    if (T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
+    const int lds = D::lds_bytes(S);
+    if (lds > 160 * 1024) return UDE_E_UNSUPPORTED;
+    static bool done = false;
+    if (!done) {
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_loss_kernel<D, M::L, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_loss_kernel<D, M::L, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      done = true;
+    }
+    int cus = 0, occ = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, true>, NTHREADS, lds));
+    if (occ < 1) occ = 1;
+    const long mx = (long)cus * occ, groups = (long)T * B;
+    *g = (int)(groups < mx ? groups : mx);
+    return UDE_OK;
+  }
+  static Layout layout(int T, int B, int g) {
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    Layout L;
+    L.musd = 0;
+    L.part = al((size_t)T * B * M::R * 2 * 4);
+    L.slab = L.part + al((size_t)g * 2 * 8);
+    L.total = L.slab + al((size_t)g * D::SLAB * 4);
+    return L;
+  }
+  static int workspace(int T, int S, int B, int device, int64_t* bytes) {
+    int g = 1;
+    int rc = grid(device, T, S, B, &g);
+    if (rc) return rc;
+    *bytes = (int64_t)layout(T, B, g).total;
+    return UDE_OK;
+  }
+  static int run(bool bwd, int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
+                 const float* grad, void* ws, float* out, float* dlatent, float* dW, float* db, hipStream_t s) {
+    if (!latent || !W || !b || !y || !ws) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    int g = 1;
+    int rc = grid(dev, T, S, B, &g);
+    if (rc) return rc;
+    const Layout Lo = layout(T, B, g);
+    unsigned char* base = (unsigned char*)ws;
+    LArgs a;
+    memset(&a, 0, sizeof(a));
+    a.latent = latent; a.W = W; a.bias = b; a.y = y;
+    a.musd = (float*)(base + Lo.musd); a.part = (double*)(base + Lo.part); a.slab = (float*)(base + Lo.slab);
+    a.dlatent = dlatent; a.grad = grad;
+    a.T = T; a.S = S; a.B = B;
+    const int lds = D::lds_bytes(S);
+    if (!bwd) {
+      if (!out) return UDE_E_INVALID;
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, false>), dim3(g), dim3(NTHREADS), lds, s, a);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL(ude_loss_finalize_kernel<0>, dim3(1), dim3(128), 0, s, (const double*)a.part, g,
+                         (double)B * T * M::R, out);
+      HIPCHK(hipGetLastError());
+    } else {
+      if (!grad || !dlatent || !dW || !db) return UDE_E_INVALID;
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, true>), dim3(g), dim3(NTHREADS), lds, s, a);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((ude_loss_grad_finalize_kernel<D>), dim3((D::SLAB + 255) / 256), dim3(256), 0, s,
+                         (const float*)a.slab, g, dW, db);
+      HIPCHK(hipGetLastError());
+    }
+    return UDE_OK;
+  }
+  static int forward(int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
+                     void* ws, float* out, hipStream_t s) {
+    return run(false, T, S, B, latent, W, b, y, nullptr, ws, out, nullptr, nullptr, nullptr, s);
+  }
+  static int backward(int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
+                      const float* grad, void* ws, float* dlatent, float* dW, float* db, hipStream_t s) {
+    return run(true, T, S, B, latent, W, b, y, grad, ws, nullptr, dlatent, dW, db, s);
+  }
+};
+
 struct Entry {
   bool (*match)(const UdeModelDesc*);
   int (*query)(const UdeProblem*, int, UdeSizes*);
@@ -346,12 +432,18 @@ struct Entry {
   int (*dopri5_workspace)(const UdeProblem*, int, int64_t*);
   int (*dopri5_forward)(const UdeProblem*, const float*, const double*, double, double, double, int, const float*,
                         float*, void*, float*, UdeDopriInfo*, hipStream_t);
+  int (*loss_workspace)(int, int, int, int, int64_t*);
+  int (*loss_forward)(int, int, int, const float*, const float*, const float*, const float*, void*, float*,
+                      hipStream_t);
+  int (*loss_backward)(int, int, int, const float*, const float*, const float*, const float*, const float*, void*,
+                       float*, float*, float*, hipStream_t);
 };
 
 template <class M>
 constexpr Entry make_entry() {
   return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward,
-               &DopriOps<M>::workspace, &DopriOps<M>::forward};
+               &DopriOps<M>::workspace, &DopriOps<M>::forward, &LossOps<M>::workspace, &LossOps<M>::forward,
+               &LossOps<M>::backward};
 }
 
 

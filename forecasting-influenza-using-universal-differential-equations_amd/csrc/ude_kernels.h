@@ -1468,14 +1468,45 @@ __global__ __launch_bounds__(256) void ude_static_reduce_kernel(const float* __r
 // d y0[:, static] = G0[tile]^T (16 x K0) x W0SP (K0 x S16) on MFMA, plus the direct
 // cotangents of every output time (static latent dims are carried unchanged).
 // One workgroup per trajectory tile; wave w owns static column tiles w, w + 4, ...
+// The time sums read the tile's contiguous (16, R, L) block of every output time
+// (coalesced, all dims) into LDS first: the static dims alone are a 5-of-8 stride.
 template <class M>
 __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __restrict__ g0buf,
                                                              const float* __restrict__ pack,
                                                              const float* __restrict__ dlatent, int n_traj,
                                                              int n_times, float* __restrict__ dy0) {
-  constexpr int NST = M::S16 / 16, SPW = (NST + 3) / 4;
+  extern __shared__ float tsum[];                    // [TT][R][L] time sums of d latent
+  constexpr int NST = M::S16 / 16, SPW = (NST + 3) / 4, BLK = TT * M::R * M::L;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
   const int tile = blockIdx.x;
+  const size_t NRL = (size_t)n_traj * M::R * M::L;
+  {
+    const int nvalid = min(TT, n_traj - tile * TT) * M::R * M::L;
+    const float* blk = dlatent + (size_t)tile * BLK;
+    if constexpr ((M::R * M::L) % 4 == 0) {
+      // 16-B loads, 8 output times in flight per lane (the sums stay in time order)
+      #pragma unroll 1
+      for (int i = 4 * threadIdx.x; i < BLK; i += 4 * 256) {
+        f4 v = f4zero();
+        if (i < nvalid) {
+#pragma unroll 8
+          for (int jt = 0; jt < n_times; ++jt) v += *reinterpret_cast<const f4*>(blk + (size_t)jt * NRL + i);
+        }
+        *reinterpret_cast<f4*>(tsum + i) = v;
+      }
+    } else {
+      #pragma unroll 1
+      for (int i = threadIdx.x; i < BLK; i += 256) {
+        float v = 0.f;
+        if (i < nvalid) {
+#pragma unroll 8
+          for (int jt = 0; jt < n_times; ++jt) v += blk[(size_t)jt * NRL + i];
+        }
+        tsum[i] = v;
+      }
+    }
+  }
+  __syncthreads();
   const float* gb = g0buf + (size_t)tile * M::K0 * TT;
   const float* wp = pack + M::W0SP_OFF;
   f4 acc[SPW];
@@ -1488,30 +1519,17 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
     for (int j = 0; j < SPW; ++j)
       if (w + 4 * j < NST) acc[j] = mfma4(a, wp[(4 * q + g) * M::S16 + (w + 4 * j) * 16 + t], acc[j]);
   }
-  const size_t NRL = (size_t)n_traj * M::R * M::L;
 #pragma unroll
   for (int j = 0; j < SPW; ++j) {
     const int s = (w + 4 * j) * 16 + t;
     if (w + 4 * j >= NST || s >= M::S) continue;
     const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
-    // the 4 trajectories' cotangent streams are summed side by side (time order per
-    // element); unrolled so a few dozen HBM loads are in flight per lane
-    size_t base[4];
-    f4 v = acc[j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int n = min(tile * TT + 4 * g + e, n_traj - 1);
-      base[e] = ((size_t)n * M::R + r) * M::L + 3 + cc;
+      const int n = tile * TT + 4 * g + e;
+      if (n < n_traj)
+        dy0[((size_t)n * M::R + r) * M::L + 3 + cc] = acc[j][e] + tsum[((4 * g + e) * M::R + r) * M::L + 3 + cc];
     }
-#pragma unroll 4
-    for (int jt = 0; jt < n_times; ++jt) {
-      const float* dl = dlatent + (size_t)jt * NRL;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += dl[base[e]];
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (tile * TT + 4 * g + e < n_traj) dy0[base[e]] = v[e];
   }
 }
 

@@ -88,6 +88,28 @@ int ude_dopri5_forward(const UdeModelDesc* m, const UdeProblem* p, const float* 
                            (hipStream_t)stream);
 }
 
+int ude_loss_head_workspace(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, int device, int64_t* ws_bytes) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!ws_bytes) return UDE_E_INVALID;
+  return e->loss_workspace(T, S, B, device, ws_bytes);
+}
+
+int ude_loss_head_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                          const float* W, const float* b, const float* y, void* ws, float* out, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  return e->loss_forward(T, S, B, latent, W, b, y, ws, out, (hipStream_t)stream);
+}
+
+int ude_loss_head_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                           const float* W, const float* b, const float* y, const float* grad, void* ws,
+                           float* dlatent, float* dW, float* db, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  return e->loss_backward(T, S, B, latent, W, b, y, grad, ws, dlatent, dW, db, (hipStream_t)stream);
+}
+
 #ifdef UDE_PROFILE
 void ude_debug_set_prof(unsigned long long* p) { ude::g_prof_buffer = p; }
 #endif

@@ -7,6 +7,9 @@ when the model lives on a HIP device -- then decodes ``latent[..., :3]``.
 ``calc_loss`` (:142-198) reads the solver's side outputs exactly as the
 reference does (``ode.posterior()``, ``torch.norm(torch.stack(ode.tracker))``,
 ``self.latent``) and ``train_step`` (:200-223) back-propagates through the solve.
+On a HIP device the ``nll`` and ``reg_loss`` terms of the model's own training
+prediction come from the fused loss head (ude_amd/loss_head.py: decoder +
+nll_loss + latent_init_loss, forward and backward in one kernel pass each).
 """
 from itertools import chain
 
@@ -21,6 +24,7 @@ import lib.Metrics as Metrics
 import lib.models as models
 import lib.train_functions as train_functions
 from lib.in_development.models_bayes import Dense_Variational
+from ude_amd import loss_head
 
 
 def warm_up_lr(epoch):
@@ -113,7 +117,23 @@ class VAE:
                 z = (models.reparam(eps, None, self.mean, n_samples, B, uncertainty=False) + 1e-5).unsqueeze(1)
             self.latent = odeint(self.ode, z, t, method="rk4", options=dict(step_size=step))
             decoded = self.dec(self.latent[..., :3])
-            return decoded.reshape((-1, n_samples, B, self.n_regions)).permute(2, 1, 0, 3)
+            y_pred = decoded.reshape((-1, n_samples, B, self.n_regions)).permute(2, 1, 0, 3)
+        # calc_loss may take nll / reg from the fused loss head when handed this prediction
+        self._pred_src = (y_pred, n_samples, B) if training else None
+        return y_pred
+
+    def _fused_head(self, y_pred, y_true, losses):
+        """(nll, reg) from the fused gfx950 loss head (ude_amd/loss_head.py), or None when
+        y_pred is not this model's latest training prediction or the shapes do not fit."""
+        src = getattr(self, "_pred_src", None)
+        if not (losses.get("nll", True) or losses.get("reg_loss", True)) or src is None or src[0] is not y_pred:
+            return None
+        lin = self.dec.decoder[-1]
+        if getattr(self.dec, "latent_dim", None) != 3 or not hasattr(self.ode, "ude_config"):
+            return None
+        if not loss_head.eligible(self.ode, self.latent, lin, src[1], src[2]):
+            return None
+        return loss_head.fused_loss_head(self.ode, self.latent, lin, y_true, src[1], src[2])
 
     def calc_loss(self, y_pred, y_true, losses):
         terms = {}
@@ -122,8 +142,9 @@ class VAE:
             self.kl_w = train_functions.KL_annealing(self.tr_step, self.anneal_params)
         if losses.get("mse", True):
             terms["mse"] = torch.mean(torch.square(y_pred - y_true.unsqueeze(1)))
+        fused = self._fused_head(y_pred, y_true, losses)
         if losses.get("nll", True):
-            terms["nll"] = train_functions.nll_loss(y_pred, y_true)
+            terms["nll"] = fused[0] if fused is not None else train_functions.nll_loss(y_pred, y_true)
         if losses.get("kl_z", True):
             prior = models.make_prior(self.mean, latent_dim=self.ld_ode, device=self.device)
             kl = train_functions.kl_divergence(prior, Normal(self.mean, self.std)).sum(-1).mean()
@@ -137,7 +158,8 @@ class VAE:
             norm = torch.norm(torch.stack(self.ode.tracker))
             terms["Fa_norm"] = losses["Fa_norm"] * norm
         if losses.get("reg_loss", True):
-            terms["reg_loss"] = 0.1 * train_functions.latent_init_loss(self.latent[..., :3])
+            terms["reg_loss"] = 0.1 * (fused[1] if fused is not None
+                                       else train_functions.latent_init_loss(self.latent[..., :3]))
         if self.ode.uncertainty == "bayes":
             terms["ode_kl"] = self.ode_kl_w * self.ode.get_kl()
         loss = torch.tensor(0.0, requires_grad=True)

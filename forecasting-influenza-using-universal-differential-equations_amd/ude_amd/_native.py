@@ -37,6 +37,7 @@ _ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "i
 
 EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_weights_bayes",
                     "ude_rk4_forward", "ude_rk4_backward", "ude_dopri5_workspace", "ude_dopri5_forward",
+                    "ude_loss_head_workspace", "ude_loss_head_forward", "ude_loss_head_backward",
                     "ude_build_info")
 
 
@@ -117,6 +118,12 @@ class NativeLib:
         L.ude_dopri5_forward.argtypes = [pdesc, pprob, vp, vp, dbl, dbl, dbl, ctypes.c_int32, vp, vp, vp, vp,
                                          ctypes.POINTER(UdeDopriInfo), vp]
         L.ude_dopri5_forward.restype = i32
+        L.ude_loss_head_workspace.argtypes = [pdesc, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_int64)]
+        L.ude_loss_head_workspace.restype = i32
+        L.ude_loss_head_forward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_loss_head_forward.restype = i32
+        L.ude_loss_head_backward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_loss_head_backward.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -169,6 +176,20 @@ class NativeLib:
                                  f"(after {info.n_steps} steps, {info.n_evals} evaluations)")
         check(rc, "ude_dopri5_forward")
         return info
+
+    def loss_workspace(self, desc, T, S, B, device) -> int:
+        out = ctypes.c_int64(0)
+        check(self.lib.ude_loss_head_workspace(ctypes.byref(desc), int(T), int(S), int(B), int(device),
+                                               ctypes.byref(out)), "ude_loss_head_workspace")
+        return int(out.value)
+
+    def loss_forward(self, desc, T, S, B, latent, W, b, y, ws, out, stream) -> None:
+        check(self.lib.ude_loss_head_forward(ctypes.byref(desc), int(T), int(S), int(B), latent, W, b, y, ws, out,
+                                             stream), "ude_loss_head_forward")
+
+    def loss_backward(self, desc, T, S, B, latent, W, b, y, grad, ws, dlat, dW, db, stream) -> None:
+        check(self.lib.ude_loss_head_backward(ctypes.byref(desc), int(T), int(S), int(B), latent, W, b, y, grad,
+                                              ws, dlat, dW, db, stream), "ude_loss_head_backward")
 
     def build_info(self) -> str:
         return self.lib.ude_build_info().decode()

@@ -160,6 +160,27 @@ int ude_dopri5_forward(const UdeModelDesc* m, const UdeProblem* p, const float* 
                        double rtol, double atol, double first_step, int32_t max_steps, const float* y0,
                        float* latent, void* ws, float* stats_out, UdeDopriInfo* info, ude_stream_t stream);
 
+/* ---- fused loss head ----------------------------------------------------------
+ * The training loss terms that read the solve's latent, forward and backward in one
+ * pass each over it (replaces, for one model's R and L):
+ *   y_pred = Decoder(latent[..., :3])  (lib/models.py:27-51, Linear(3R -> R); lib/VAE.py:138)
+ *            reshaped (T, S, B, R) -> permuted (B, S, T, R), sample n = s * B + b
+ *   out[0] = nll_loss(y_pred, y)       (lib/train_functions.py:81-90: mean / unbiased std
+ *            over the S samples, -Normal.log_prob(y), zero where y == -1, mean over B*T*R)
+ *   out[1] = latent_init_loss(latent[..., :3])  (lib/train_functions.py:116-126, a sum)
+ * latent (T, S*B, R, L), W (R, 3R), b (R), y (B, T, R); S >= 2.  ws: workspace bytes
+ * from ude_loss_head_workspace, kept from forward to backward (per-group mean / std).
+ * backward: grad (device, 2 floats) = d loss / d out; writes dlatent (T, S*B, R, L)
+ * (dims >= 3: zero), dW (R, 3R), db (R). */
+int ude_loss_head_workspace(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, int device, int64_t* ws_bytes);
+
+int ude_loss_head_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                          const float* W, const float* b, const float* y, void* ws, float* out, ude_stream_t stream);
+
+int ude_loss_head_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                           const float* W, const float* b, const float* y, const float* grad, void* ws,
+                           float* dlatent, float* dW, float* db, ude_stream_t stream);
+
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);
 

@@ -345,7 +345,7 @@ struct LossOps {
   static int grid(int device, int T, int S, int B, int* g) {
     if (T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
     const int lds = D::lds_bytes(S);
-    if (lds > 160 * 1024) return UDE_E_UNSUPPORTED;
+    if (lds > 160 * 1024 || pad16(S) > SP_MAX) return UDE_E_UNSUPPORTED;
     static bool done = false;
     if (!done) {
       HIPCHK(hipFuncSetAttribute((const void*)&ude_loss_kernel<D, M::L, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

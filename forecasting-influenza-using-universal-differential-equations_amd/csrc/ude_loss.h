@@ -14,6 +14,8 @@
 
 namespace ude {
 
+constexpr int SP_MAX = 128;                  // samples per group the loss head holds (LDS)
+
 template <int R_>
 struct LossDims {
   static constexpr int R = R_;
@@ -80,16 +82,37 @@ __device__ void loss_body(const LArgs& A, float* lds) {
   for (int grp = blockIdx.x; grp < A.T * A.B; grp += gridDim.x) {
     const int t = grp / A.B, b = grp - t * A.B;
     // ---- the group's S sample rows (dims 0..2 of every region) -> X ----------------
+    // zero the padding (rows >= S, columns >= 3R), then stream whole rows (R*L floats,
+    // contiguous) with 16-B loads and keep the dynamic dims
     #pragma unroll 1
     for (int i = tid; i < SP * D::XS; i += NTHREADS) {
       const int s = i / D::XS, k = i - s * D::XS;
-      float v = 0.f;
-      if (s < S && k < D::K) {
-        const int r = k / 3, c = k - 3 * r;
-        v = A.latent[(size_t)t * NRL + ((size_t)(s * A.B + b) * D::R + r) * L + c];
-        if (!BWD) reg_acc += (double)((v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f));
+      if (s >= S || k >= D::K) X[i] = 0.f;
+    }
+    if constexpr ((D::R * L) % 4 == 0) {
+      constexpr int RL4 = D::R * L / 4;
+      const int n4 = S * RL4;
+#pragma unroll 4
+      for (int i = tid; i < n4; i += NTHREADS) {
+        const int s = i / RL4, j = i - s * RL4;
+        const f4 v = *reinterpret_cast<const f4*>(A.latent + (size_t)t * NRL + (size_t)(s * A.B + b) * D::R * L + 4 * j);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = 4 * j + q, r = e / L, c = e - r * L;
+          if (c < 3) {
+            X[s * D::XS + 3 * r + c] = v[q];
+            if (!BWD) reg_acc += (double)((v[q] < 0.f ? fabsf(v[q]) : 0.f) + (v[q] > 1.f ? fabsf(1.f - v[q]) : 0.f));
+          }
+        }
       }
-      X[i] = v;
+    } else {
+      #pragma unroll 4
+      for (int i = tid; i < S * D::K; i += NTHREADS) {
+        const int s = i / D::K, k = i - s * D::K, r = k / 3, c = k - 3 * r;
+        const float v = A.latent[(size_t)t * NRL + ((size_t)(s * A.B + b) * D::R + r) * L + c];
+        if (!BWD) reg_acc += (double)((v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f));
+        X[s * D::XS + k] = v;
+      }
     }
     __syncthreads();
     // ---- P = X W^T + b  (S x R) ----------------------------------------------------
@@ -152,38 +175,7 @@ __device__ void loss_body(const LArgs& A, float* lds) {
         Q[s * D::PS + r] = 0.f;
       }
       __syncthreads();
-      // ---- d X = Q W  (S x 3R) -> d latent (+ g_reg * latent_init_loss'), full rows --
-      for (int mt = W; mt < SP / 16; mt += WAVES) {
-        f4 acc[D::KT];
-#pragma unroll
-        for (int kt = 0; kt < D::KT; ++kt) acc[kt] = f4zero();
-#pragma unroll 4
-        for (int rq = 0; rq < D::NP / 4; ++rq) {
-          const float a = Q[(mt * 16 + t16) * D::PS + 4 * rq + g];
-#pragma unroll
-          for (int kt = 0; kt < D::KT; ++kt) acc[kt] = mfma4(a, Wl[(4 * rq + g) * D::XS + kt * 16 + t16], acc[kt]);
-        }
-#pragma unroll
-        for (int kt = 0; kt < D::KT; ++kt)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int s = mt * 16 + 4 * g + e, k = kt * 16 + t16;
-            if (s < S && k < D::K) {
-              const float x = X[s * D::XS + k];
-              const float dr = x < 0.f ? -1.f : (x > 1.f ? 1.f : 0.f);
-              const int r = k / 3, c = k - 3 * r;
-              A.dlatent[(size_t)t * NRL + ((size_t)(s * A.B + b) * D::R + r) * L + c] = acc[kt][e] + g_reg * dr;
-            }
-          }
-      }
-      // static dims (3 .. L-1) of the group's rows get no gradient from the loss head
-      if constexpr (L > 3) {
-        for (int i = tid; i < S * D::R * (L - 3); i += NTHREADS) {
-          const int s = i / (D::R * (L - 3)), rem = i - s * D::R * (L - 3), r = rem / (L - 3), c = 3 + rem - r * (L - 3);
-          A.dlatent[(size_t)t * NRL + ((size_t)(s * A.B + b) * D::R + r) * L + c] = 0.f;
-        }
-      }
-      // ---- dW += Q^T X (R x 3R), db += sum_s Q ------------------------------------
+      // ---- dW += Q^T X (R x 3R) ----------------------------------------------------
 #pragma unroll
       for (int i = 0; i < D::tiles_of(W); ++i) {
         const int id = W + WAVES * i, nt = id / D::KT, kt = id - nt * D::KT;
@@ -191,6 +183,61 @@ __device__ void loss_body(const LArgs& A, float* lds) {
         for (int sq = 0; sq < SP / 4; ++sq)
           acc = mfma4(Q[(4 * sq + g) * D::PS + nt * 16 + t16], X[(4 * sq + g) * D::XS + kt * 16 + t16], acc);
         dw[i] = acc;
+      }
+      // ---- d X = Q W  (S x 3R), + g_reg * latent_init_loss'(x), in place of X ----------
+      // (every wave first finishes reading X / Q; each M tile is owned by one wave)
+      constexpr int MI = (SP_MAX / 16 + WAVES - 1) / WAVES;
+      f4 dx[MI][D::KT];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int mt = W + WAVES * mi;
+        if (mt < SP / 16) {
+#pragma unroll
+          for (int kt = 0; kt < D::KT; ++kt) dx[mi][kt] = f4zero();
+#pragma unroll 4
+          for (int rq = 0; rq < D::NP / 4; ++rq) {
+            const float a = Q[(mt * 16 + t16) * D::PS + 4 * rq + g];
+#pragma unroll
+            for (int kt = 0; kt < D::KT; ++kt) dx[mi][kt] = mfma4(a, Wl[(4 * rq + g) * D::XS + kt * 16 + t16], dx[mi][kt]);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int mt = W + WAVES * mi;
+        if (mt < SP / 16)
+#pragma unroll
+          for (int kt = 0; kt < D::KT; ++kt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float* xp = X + (mt * 16 + 4 * g + e) * D::XS + kt * 16 + t16;
+              const float x = *xp;
+              const float dr = x < 0.f ? -1.f : (x > 1.f ? 1.f : 0.f);
+              *xp = dx[mi][kt][e] + g_reg * dr;
+            }
+      }
+      __syncthreads();
+      // ---- whole rows of d latent (static dims 0) with 16-B stores ---------------------
+      if constexpr ((D::R * L) % 4 == 0) {
+        constexpr int RL4 = D::R * L / 4;
+#pragma unroll 4
+        for (int i = tid; i < S * RL4; i += NTHREADS) {
+          const int s = i / RL4, j = i - s * RL4;
+          f4 v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = 4 * j + q, r = e / L, c = e - r * L;
+            v[q] = c < 3 ? X[s * D::XS + 3 * r + c] : 0.f;
+          }
+          *reinterpret_cast<f4*>(A.dlatent + (size_t)t * NRL + (size_t)(s * A.B + b) * D::R * L + 4 * j) = v;
+        }
+      } else {
+        #pragma unroll 4
+        for (int i = tid; i < S * D::R * L; i += NTHREADS) {
+          const int s = i / (D::R * L), e = i - s * D::R * L, r = e / L, c = e - r * L;
+          A.dlatent[(size_t)t * NRL + (size_t)(s * A.B + b) * D::R * L + e] = c < 3 ? X[s * D::XS + 3 * r + c] : 0.f;
+        }
       }
       for (int r = tid; r < D::NP; r += NTHREADS) {
         float s1 = 0.f;

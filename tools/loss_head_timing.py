@@ -18,3 +18,14 @@ for _ in range(3): step()
 torch.cuda.synchronize(); t0 = time.perf_counter()
 for _ in range(20): step()
 torch.cuda.synchronize(); print("loss head fwd+bwd ms", (time.perf_counter() - t0) / 20 * 1e3)
+from ude_amd import loss_head
+ode = importlib.import_module("forecasting-influenza-using-universal-differential-equations_amd").FaFp(
+    R, latent_dim=L, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]).to(dev)
+lin = dec.decoder[-1]
+def fstep():
+    nll, reg = loss_head.fused_loss_head(ode, lat, lin, y, S, B)
+    (nll + 0.1 * reg).backward()
+for _ in range(3): fstep()
+torch.cuda.synchronize(); t0 = time.perf_counter()
+for _ in range(20): fstep()
+torch.cuda.synchronize(); print("fused loss head fwd+bwd ms", (time.perf_counter() - t0) / 20 * 1e3)

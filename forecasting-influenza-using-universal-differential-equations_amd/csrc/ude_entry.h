@@ -354,7 +354,7 @@ struct LossOps {
     }
     int cus = 0, occ = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, true>, NTHREADS, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, true>, LTHREADS, lds));
     if (occ < 1) occ = 1;
     const long mx = (long)cus * occ, groups = (long)T * B;
     *g = (int)(groups < mx ? groups : mx);
@@ -395,16 +395,16 @@ struct LossOps {
     const int lds = D::lds_bytes(S);
     if (!bwd) {
       if (!out) return UDE_E_INVALID;
-      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, false>), dim3(g), dim3(NTHREADS), lds, s, a);
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, false>), dim3(g), dim3(LTHREADS), lds, s, a);
       HIPCHK(hipGetLastError());
       hipLaunchKernelGGL(ude_loss_finalize_kernel<0>, dim3(1), dim3(128), 0, s, (const double*)a.part, g,
                          (double)B * T * M::R, out);
       HIPCHK(hipGetLastError());
     } else {
       if (!grad || !dlatent || !dW || !db) return UDE_E_INVALID;
-      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, true>), dim3(g), dim3(NTHREADS), lds, s, a);
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, true>), dim3(g), dim3(LTHREADS), lds, s, a);
       HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((ude_loss_grad_finalize_kernel<D>), dim3((D::SLAB + 255) / 256), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_loss_grad_finalize_kernel<D>), dim3((D::SLAB + 63) / 64), dim3(256), 0, s,
                          (const float*)a.slab, g, dW, db);
       HIPCHK(hipGetLastError());
     }

@@ -15,6 +15,8 @@
 namespace ude {
 
 constexpr int SP_MAX = 128;                  // samples per group the loss head holds (LDS)
+constexpr int LWAVES = 8;                    // loss-head waves per workgroup (two per SIMD)
+constexpr int LTHREADS = LWAVES * 64;
 
 template <int R_>
 struct LossDims {
@@ -26,11 +28,12 @@ struct LossDims {
   static constexpr int XS = KP + 4;          // LDS row strides (== 4 mod 64 floats where possible)
   static constexpr int PS = NP + 4;
   static constexpr int NTILE = NT * KT;      // dW tiles (16 x 16)
-  static constexpr int tiles_of(int w) { return (NTILE + WAVES - 1 - w) / WAVES; }
+  static constexpr int tiles_of(int w) { return (NTILE + LWAVES - 1 - w) / LWAVES; }
   static constexpr int SLAB = NP * KP + NP;  // per-workgroup dW | db partials
+  static_assert(NP <= LTHREADS / 4, "one lane quad per decoder output");
   static int lds_bytes(int S) {
     const int SP = pad16(S);
-    return (SP * XS + NP * XS + 2 * SP * PS + 2 * NP) * 4;
+    return (SP * XS + NP * XS + SP * PS + 2 * NP) * 4;
   }
 };
 
@@ -47,7 +50,22 @@ struct LArgs {
   int T, S, B;
 };
 
-// LDS layout: X [SP][XS] | Wl [NP][XS] | P [SP][PS] | Q [SP][PS] | bias [NP] | aux [NP]
+// barrier for LDS hand-offs only: in-flight global loads (the next group's prefetch)
+// stay in flight across it
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ float reg_term(float v) {
+  return (v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f);
+}
+
+// LDS layout: X [SP][XS] | Wl [NP][XS] | P [SP][PS] (Q in place, backward) | bias [NP] | aux [NP]
+// A group's rows are read once: when L % 4 == 0 the dims 0..3 of every (sample, region)
+// are one 16-B load, and the next group's loads are issued into registers before the
+// current group's GEMMs run (software pipelined across the group loop).
 template <class D, int L, bool BWD, int W>
 __device__ void loss_body(const LArgs& A, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, t16 = lane & 15, g = lane >> 4;
@@ -55,19 +73,21 @@ __device__ void loss_body(const LArgs& A, float* lds) {
   float* X = lds;
   float* Wl = X + SP * D::XS;
   float* P = Wl + D::NP * D::XS;
-  float* Q = P + SP * D::PS;
-  float* bl = Q + SP * D::PS;
+  float* bl = P + SP * D::PS;
   const size_t NRL = (size_t)N * D::R * L;
   const double M = (double)A.B * A.T * D::R;    // nll.mean() over (B, T, R)
   const float g_nll = BWD ? A.grad[0] : 0.f, g_reg = BWD ? A.grad[1] : 0.f;
+  const int ngroups = A.T * A.B;
 
-  // decoder weight / bias -> LDS (zero padded), once per workgroup
+  // decoder weight / bias -> LDS (zero padded), X padding zeroed, once per workgroup
   #pragma unroll 1
-  for (int i = tid; i < D::NP * D::XS; i += NTHREADS) {
+  for (int i = tid; i < D::NP * D::XS; i += LTHREADS) {
     const int o = i / D::XS, k = i - o * D::XS;
     Wl[i] = (o < D::R && k < D::K) ? A.W[o * D::K + k] : 0.f;
   }
-  for (int i = tid; i < D::NP; i += NTHREADS) {
+  #pragma unroll 1
+  for (int i = tid; i < SP * D::XS; i += LTHREADS) X[i] = 0.f;
+  for (int i = tid; i < D::NP; i += LTHREADS) {
     bl[i] = i < D::R ? A.bias[i] : 0.f;
     bl[D::NP + i] = 0.f;                         // db partial (backward)
   }
@@ -77,88 +97,107 @@ __device__ void loss_body(const LArgs& A, float* lds) {
     for (int i = 0; i < D::tiles_of(W); ++i) dw[i] = f4zero();
   }
   double nll_acc = 0.0, reg_acc = 0.0;
+
+  constexpr bool VEC = (L % 4) == 0;
+  constexpr int PF = VEC ? (SP_MAX * D::R + LTHREADS - 1) / LTHREADS : 1;
+  const int nreg = S * D::R;                     // (sample, region) pairs of a group
+  f4 pf[PF];
+  auto prefetch = [&](int grp) {
+    const int t = grp / A.B, b = grp - t * A.B;
+    const float* base = A.latent + (size_t)t * NRL;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      if (j * LTHREADS < nreg) {
+        int i = tid + j * LTHREADS;
+        i = i < nreg ? i : nreg - 1;
+        const int s = i / D::R, r = i - s * D::R;
+        pf[j] = *reinterpret_cast<const f4*>(base + ((size_t)(s * A.B + b) * D::R + r) * L);
+      }
+    }
+  };
+  if constexpr (VEC) {
+    if ((int)blockIdx.x < ngroups) prefetch(blockIdx.x);
+  }
   __syncthreads();
 
-  for (int grp = blockIdx.x; grp < A.T * A.B; grp += gridDim.x) {
+  #pragma unroll 1
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int t = grp / A.B, b = grp - t * A.B;
     // ---- the group's S sample rows (dims 0..2 of every region) -> X ----------------
-    // zero the padding (rows >= S, columns >= 3R), then stream whole rows (R*L floats,
-    // contiguous) with 16-B loads and keep the dynamic dims
-    #pragma unroll 1
-    for (int i = tid; i < SP * D::XS; i += NTHREADS) {
-      const int s = i / D::XS, k = i - s * D::XS;
-      if (s >= S || k >= D::K) X[i] = 0.f;
-    }
-    if constexpr ((D::R * L) % 4 == 0) {
-      constexpr int RL4 = D::R * L / 4;
-      const int n4 = S * RL4;
-#pragma unroll 4
-      for (int i = tid; i < n4; i += NTHREADS) {
-        const int s = i / RL4, j = i - s * RL4;
-        const f4 v = *reinterpret_cast<const f4*>(A.latent + (size_t)t * NRL + (size_t)(s * A.B + b) * D::R * L + 4 * j);
+    if constexpr (VEC) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = 4 * j + q, r = e / L, c = e - r * L;
-          if (c < 3) {
-            X[s * D::XS + 3 * r + c] = v[q];
-            if (!BWD) reg_acc += (double)((v[q] < 0.f ? fabsf(v[q]) : 0.f) + (v[q] > 1.f ? fabsf(1.f - v[q]) : 0.f));
-          }
+      for (int j = 0; j < PF; ++j) {
+        const int i = tid + j * LTHREADS;
+        if (j * LTHREADS < nreg && i < nreg) {
+          const int s = i / D::R, r = i - s * D::R;
+          float* xp = X + s * D::XS + 3 * r;
+          xp[0] = pf[j][0]; xp[1] = pf[j][1]; xp[2] = pf[j][2];
+          if (!BWD) reg_acc += (double)(reg_term(pf[j][0]) + reg_term(pf[j][1]) + reg_term(pf[j][2]));
         }
       }
     } else {
       #pragma unroll 4
-      for (int i = tid; i < S * D::K; i += NTHREADS) {
+      for (int i = tid; i < S * D::K; i += LTHREADS) {
         const int s = i / D::K, k = i - s * D::K, r = k / 3, c = k - 3 * r;
         const float v = A.latent[(size_t)t * NRL + ((size_t)(s * A.B + b) * D::R + r) * L + c];
-        if (!BWD) reg_acc += (double)((v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f));
+        if (!BWD) reg_acc += (double)reg_term(v);
         X[s * D::XS + k] = v;
       }
     }
-    __syncthreads();
-    // ---- P = X W^T + b  (S x R) ----------------------------------------------------
-    for (int mt = W; mt < SP / 16; mt += WAVES) {
-      f4 acc[D::NT];
-#pragma unroll
-      for (int nt = 0; nt < D::NT; ++nt) acc[nt] = f4zero();
-#pragma unroll 4
-      for (int kq = 0; kq < D::KP / 4; ++kq) {
-        const float a = X[(mt * 16 + t16) * D::XS + 4 * kq + g];
-#pragma unroll
-        for (int nt = 0; nt < D::NT; ++nt) acc[nt] = mfma4(a, Wl[(nt * 16 + t16) * D::XS + 4 * kq + g], acc[nt]);
+    // per-region inputs of this group, loaded before the next group's prefetch
+    float yv = -1.f, mu_in = 0.f, sd_in = 1.f;
+    const int rq = tid >> 2, part = tid & 3;     // 4 lanes per region
+    if (rq < D::R) {
+      yv = A.y[((size_t)b * A.T + t) * D::R + rq];
+      if (BWD) {
+        mu_in = A.musd[(((size_t)t * A.B + b) * D::R + rq) * 2];
+        sd_in = A.musd[(((size_t)t * A.B + b) * D::R + rq) * 2 + 1];
       }
-#pragma unroll
-      for (int nt = 0; nt < D::NT; ++nt)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) P[(mt * 16 + 4 * g + e) * D::PS + nt * 16 + t16] = acc[nt][e] + bl[nt * 16 + t16];
     }
-    __syncthreads();
-    // ---- per region: mean / unbiased std over the samples; nll or d nll / d pred ---
-    for (int r = tid; r < D::R; r += NTHREADS) {
-      float mu, sd;
+    if constexpr (VEC) {
+      if (grp + (int)gridDim.x < ngroups) prefetch(grp + gridDim.x);
+    }
+    lds_barrier();
+    // ---- P = X W^T + b  (S x R), one (M, N) tile per wave step ----------------------
+    for (int id = W; id < (SP / 16) * D::NT; id += LWAVES) {
+      const int mt = id / D::NT, nt = id - mt * D::NT;
+      f4 acc = f4zero();
+#pragma unroll 8
+      for (int kq = 0; kq < D::KP / 4; ++kq)
+        acc = mfma4(X[(mt * 16 + t16) * D::XS + 4 * kq + g], Wl[(nt * 16 + t16) * D::XS + 4 * kq + g], acc);
+      const float bv = bl[nt * 16 + t16];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) P[(mt * 16 + 4 * g + e) * D::PS + nt * 16 + t16] = acc[e] + bv;
+    }
+    lds_barrier();
+    // ---- per region (4 lanes each): mean / unbiased std over the samples; nll or
+    //      d nll / d pred (in place of P) and its column sum (db) ---------------------
+    for (int r = rq; r < D::NP; r += LTHREADS / 4) {
+      const bool real = r < D::R;
+      float mu = mu_in, sd = sd_in;
       if (!BWD) {
         float s1 = 0.f;
-        for (int s = 0; s < S; ++s) s1 += P[s * D::PS + r];
+        for (int s = part; s < S; s += 4) s1 += P[s * D::PS + r];
+        s1 += __shfl_xor(s1, 1, 64);
+        s1 += __shfl_xor(s1, 2, 64);
         mu = s1 / (float)S;
         float s2 = 0.f;
-        for (int s = 0; s < S; ++s) { const float d = P[s * D::PS + r] - mu; s2 += d * d; }
+        for (int s = part; s < S; s += 4) { const float d = P[s * D::PS + r] - mu; s2 += d * d; }
+        s2 += __shfl_xor(s2, 1, 64);
+        s2 += __shfl_xor(s2, 2, 64);
         sd = sqrtf(s2 / (float)(S - 1));
-        A.musd[(((size_t)t * A.B + b) * D::R + r) * 2] = mu;
-        A.musd[(((size_t)t * A.B + b) * D::R + r) * 2 + 1] = sd;
-      } else {
-        mu = A.musd[(((size_t)t * A.B + b) * D::R + r) * 2];
-        sd = A.musd[(((size_t)t * A.B + b) * D::R + r) * 2 + 1];
-      }
-      const float yv = A.y[((size_t)b * A.T + t) * D::R + r];
-      const bool live = yv != -1.f;
-      if (!BWD) {
-        if (live) {
-          const float z = (yv - mu) / sd;
-          nll_acc += (double)(0.5f * z * z + logf(sd) + 0.9189385332046727f);
+        if (real && part == 0) {
+          A.musd[(((size_t)t * A.B + b) * D::R + r) * 2] = mu;
+          A.musd[(((size_t)t * A.B + b) * D::R + r) * 2 + 1] = sd;
+          if (yv != -1.f) {
+            const float z = (yv - mu) / sd;
+            nll_acc += (double)(0.5f * z * z + logf(sd) + 0.9189385332046727f);
+          }
         }
       } else {
         // d/d pred_s of mean_{b,t,r}(mask * (-log N(y | mu, sd)))
         float cm = 0.f, cs = 0.f;
-        if (live) {
+        if (real && yv != -1.f) {
           const float iv = 1.f / sd, dy = yv - mu;
           const float dmu = -dy * iv * iv;                          // d nll / d mu
           const float dsd = iv - dy * dy * iv * iv * iv;            // d nll / d sd
@@ -166,63 +205,67 @@ __device__ void loss_body(const LArgs& A, float* lds) {
           cm = sc * dmu / (float)S;
           cs = sc * dsd * iv / (float)(S - 1);
         }
-        for (int s = 0; s < SP; ++s) Q[s * D::PS + r] = s < S ? cm + cs * (P[s * D::PS + r] - mu) : 0.f;
+        float s1 = 0.f;
+        for (int s = part; s < SP; s += 4) {
+          const float q = s < S ? cm + cs * (P[s * D::PS + r] - mu) : 0.f;
+          P[s * D::PS + r] = q;
+          s1 += q;
+        }
+        s1 += __shfl_xor(s1, 1, 64);
+        s1 += __shfl_xor(s1, 2, 64);
+        if (part == 0) bl[D::NP + r] += s1;     // aux row: db partial
       }
     }
     if constexpr (BWD) {
-      for (int i = tid; i < SP * (D::NP - D::R); i += NTHREADS) {
-        const int s = i / (D::NP - D::R), r = D::R + i - s * (D::NP - D::R);
-        Q[s * D::PS + r] = 0.f;
-      }
-      __syncthreads();
+      lds_barrier();
       // ---- dW += Q^T X (R x 3R) ----------------------------------------------------
+#pragma unroll 1
+      for (int sq = 0; sq < SP / 4; ++sq) {
 #pragma unroll
-      for (int i = 0; i < D::tiles_of(W); ++i) {
-        const int id = W + WAVES * i, nt = id / D::KT, kt = id - nt * D::KT;
-        f4 acc = dw[i];
-        for (int sq = 0; sq < SP / 4; ++sq)
-          acc = mfma4(Q[(4 * sq + g) * D::PS + nt * 16 + t16], X[(4 * sq + g) * D::XS + kt * 16 + t16], acc);
-        dw[i] = acc;
-      }
-      // ---- d X = Q W  (S x 3R), + g_reg * latent_init_loss'(x), in place of X ----------
-      // (every wave first finishes reading X / Q; each M tile is owned by one wave)
-      constexpr int MI = (SP_MAX / 16 + WAVES - 1) / WAVES;
-      f4 dx[MI][D::KT];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int mt = W + WAVES * mi;
-        if (mt < SP / 16) {
-#pragma unroll
-          for (int kt = 0; kt < D::KT; ++kt) dx[mi][kt] = f4zero();
-#pragma unroll 4
-          for (int rq = 0; rq < D::NP / 4; ++rq) {
-            const float a = Q[(mt * 16 + t16) * D::PS + 4 * rq + g];
-#pragma unroll
-            for (int kt = 0; kt < D::KT; ++kt) dx[mi][kt] = mfma4(a, Wl[(4 * rq + g) * D::XS + kt * 16 + t16], dx[mi][kt]);
-          }
+        for (int i = 0; i < D::tiles_of(W); ++i) {   // independent chains, one per tile
+          const int id = W + LWAVES * i, nt = id / D::KT, kt = id - nt * D::KT;
+          dw[i] = mfma4(P[(4 * sq + g) * D::PS + nt * 16 + t16], X[(4 * sq + g) * D::XS + kt * 16 + t16], dw[i]);
         }
       }
-      __syncthreads();
+      // ---- d X = Q W  (S x 3R), + g_reg * latent_init_loss'(x), in place of X ----------
+      // (after every wave has finished reading X for dW; each tile is one wave's)
+      lds_barrier();
+      // tiles of this wave in chunks of CH independent MFMA chains
+      constexpr int DXT = ((SP_MAX / 16) * D::KT + LWAVES - 1) / LWAVES, CH = DXT < 3 ? DXT : 3;
+      const int ndx = (SP / 16) * D::KT;
+#pragma unroll 1
+      for (int c0 = 0; c0 < DXT && W + LWAVES * c0 < ndx; c0 += CH) {
+        f4 dx[CH];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int mt = W + WAVES * mi;
-        if (mt < SP / 16)
+        for (int i = 0; i < CH; ++i) dx[i] = f4zero();
+#pragma unroll 2
+        for (int rq4 = 0; rq4 < D::NP / 4; ++rq4) {
 #pragma unroll
-          for (int kt = 0; kt < D::KT; ++kt)
+          for (int i = 0; i < CH; ++i) {
+            const int id = W + LWAVES * (c0 + i), mt = id / D::KT, kt = id - mt * D::KT;
+            if (id < ndx)
+              dx[i] = mfma4(P[(mt * 16 + t16) * D::PS + 4 * rq4 + g], Wl[(4 * rq4 + g) * D::XS + kt * 16 + t16], dx[i]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int id = W + LWAVES * (c0 + i), mt = id / D::KT, kt = id - mt * D::KT;
+          if (id < ndx)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               float* xp = X + (mt * 16 + 4 * g + e) * D::XS + kt * 16 + t16;
               const float x = *xp;
               const float dr = x < 0.f ? -1.f : (x > 1.f ? 1.f : 0.f);
-              *xp = dx[mi][kt][e] + g_reg * dr;
+              *xp = dx[i][e] + g_reg * dr;
             }
+        }
       }
-      __syncthreads();
+      lds_barrier();
       // ---- whole rows of d latent (static dims 0) with 16-B stores ---------------------
       if constexpr ((D::R * L) % 4 == 0) {
         constexpr int RL4 = D::R * L / 4;
 #pragma unroll 4
-        for (int i = tid; i < S * RL4; i += NTHREADS) {
+        for (int i = tid; i < S * RL4; i += LTHREADS) {
           const int s = i / RL4, j = i - s * RL4;
           f4 v;
 #pragma unroll
@@ -234,50 +277,55 @@ __device__ void loss_body(const LArgs& A, float* lds) {
         }
       } else {
         #pragma unroll 4
-        for (int i = tid; i < S * D::R * L; i += NTHREADS) {
+        for (int i = tid; i < S * D::R * L; i += LTHREADS) {
           const int s = i / (D::R * L), e = i - s * D::R * L, r = e / L, c = e - r * L;
           A.dlatent[(size_t)t * NRL + (size_t)(s * A.B + b) * D::R * L + e] = c < 3 ? X[s * D::XS + 3 * r + c] : 0.f;
         }
       }
-      for (int r = tid; r < D::NP; r += NTHREADS) {
-        float s1 = 0.f;
-        for (int s = 0; s < S; ++s) s1 += Q[s * D::PS + r];
-        bl[D::NP + r] += s1;      // aux row: db partial
-      }
+      // (X padding stays zero: Q rows s >= S and W's padding columns are zero, so dX is 0
+      // there, and the next group overwrites every real entry)
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   if constexpr (BWD) {
     float* my = A.slab + (size_t)blockIdx.x * D::SLAB;
 #pragma unroll
     for (int i = 0; i < D::tiles_of(W); ++i) {
-      const int id = W + WAVES * i, nt = id / D::KT, kt = id - nt * D::KT;
+      const int id = W + LWAVES * i, nt = id / D::KT, kt = id - nt * D::KT;
 #pragma unroll
       for (int e = 0; e < 4; ++e) my[(nt * 16 + 4 * g + e) * D::KP + kt * 16 + t16] = dw[i][e];
     }
-    for (int r = tid; r < D::NP; r += NTHREADS) my[D::NP * D::KP + r] = bl[D::NP + r];
+    __syncthreads();
+    for (int r = tid; r < D::NP; r += LTHREADS) my[D::NP * D::KP + r] = bl[D::NP + r];
   } else {
     double* red = reinterpret_cast<double*>(lds);
     const double v0 = wave_sum(nll_acc), v1 = wave_sum(reg_acc);
+    __syncthreads();
     if (lane == 0) { red[(tid >> 6) * 2] = v0; red[(tid >> 6) * 2 + 1] = v1; }
     __syncthreads();
     if (tid < 2) {
       double s = 0;
-      for (int w = 0; w < WAVES; ++w) s += red[w * 2 + tid];
+      for (int w = 0; w < LWAVES; ++w) s += red[w * 2 + tid];
       A.part[(size_t)blockIdx.x * 2 + tid] = s;
     }
   }
 }
 
 template <class D, int L, bool BWD>
-__global__ __launch_bounds__(NTHREADS) void ude_loss_kernel(LArgs a) {
+__global__ __launch_bounds__(LTHREADS) void ude_loss_kernel(LArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w == 0) loss_body<D, L, BWD, 0>(a, lds);
-  else if (w == 1) loss_body<D, L, BWD, 1>(a, lds);
-  else if (w == 2) loss_body<D, L, BWD, 2>(a, lds);
-  else loss_body<D, L, BWD, 3>(a, lds);
+  switch (w) {
+    case 0: loss_body<D, L, BWD, 0>(a, lds); break;
+    case 1: loss_body<D, L, BWD, 1>(a, lds); break;
+    case 2: loss_body<D, L, BWD, 2>(a, lds); break;
+    case 3: loss_body<D, L, BWD, 3>(a, lds); break;
+    case 4: loss_body<D, L, BWD, 4>(a, lds); break;
+    case 5: loss_body<D, L, BWD, 5>(a, lds); break;
+    case 6: loss_body<D, L, BWD, 6>(a, lds); break;
+    default: loss_body<D, L, BWD, 7>(a, lds); break;
+  }
 }
 
 // nll = sum / (B T R), reg = sum (fixed-order sums over the workgroup partials)
@@ -296,20 +344,34 @@ __global__ void ude_loss_finalize_kernel(const double* __restrict__ part, int gr
   if (threadIdx.x == 0) { out[0] = (float)(tot[0] / M); out[1] = (float)tot[1]; }
 }
 
-// sum of the per-workgroup dW / db slabs -> (R, 3R) weight gradient and (R) bias gradient
+// sum of the per-workgroup dW / db slabs -> (R, 3R) weight gradient and (R) bias gradient:
+// a block owns 64 slab columns; its 4 waves sum interleaved quarters of the slabs with 8
+// independent accumulators each, then a fixed-order combine in LDS (deterministic)
 template <class D>
 __global__ __launch_bounds__(256) void ude_loss_grad_finalize_kernel(const float* __restrict__ slab, int grid,
                                                                      float* __restrict__ dW, float* __restrict__ db) {
-  const int off = blockIdx.x * 256 + threadIdx.x;
-  if (off >= D::SLAB) return;
-  float v = 0.f;
-  for (int i = 0; i < grid; ++i) v += slab[(size_t)i * D::SLAB + off];
-  if (off < D::NP * D::KP) {
-    const int o = off / D::KP, k = off - o * D::KP;
-    if (o < D::R && k < D::K) dW[o * D::K + k] = v;
-  } else {
-    const int o = off - D::NP * D::KP;
-    if (o < D::R) db[o] = v;
+  __shared__ float red[4][64];
+  const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int off = blockIdx.x * 64 + ln;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (off < D::SLAB) {
+    int i = wv;
+    for (; i + 28 < grid; i += 32)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += slab[(size_t)(i + 4 * u) * D::SLAB + off];
+    for (; i < grid; i += 4) acc[0] += slab[(size_t)i * D::SLAB + off];
+  }
+  red[wv][ln] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (wv == 0 && off < D::SLAB) {
+    const float v = (red[0][ln] + red[1][ln]) + (red[2][ln] + red[3][ln]);
+    if (off < D::NP * D::KP) {
+      const int o = off / D::KP, k = off - o * D::KP;
+      if (o < D::R && k < D::K) dW[o * D::K + k] = v;
+    } else {
+      const int o = off - D::NP * D::KP;
+      if (o < D::R) db[o] = v;
+    }
   }
 }
 

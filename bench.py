@@ -201,6 +201,63 @@ def dopri5_line(pkg, w, dev, reps=3):
             "traj_accepted_steps_per_s": info["n_accepted"] * w["n_traj"] / el}
 
 
+def loss_head_line(pkg, w, dev, reps=20):
+    """the training loss head over the state49 solve's latent (T = 9 outputs,
+    64 MC samples x 320 windows, R = 49, L = 8): Decoder(latent[..., :3]) + nll_loss +
+    latent_init_loss, forward and backward, fused (csrc/ude_loss.h) vs the reference's own
+    torch ops on the same GPU.  HBM roofline: the fused pass reads the latent once (forward)
+    and reads it + writes d latent once (backward)."""
+    import lib.models as models
+    import lib.train_functions as tf
+    from ude_amd import fused, loss_head
+    T, S, B, R, L = 9, 64, w["n_traj"] // 64, w["R"], w["L"]
+    gen = torch.Generator(device=dev).manual_seed(5)
+    lat = torch.rand(T, S * B, R, L, device=dev, generator=gen).requires_grad_(True)
+    dec = models.Decoder(R, L, 1).to(dev)
+    y = torch.rand(B, T, R, device=dev, generator=gen)
+    ode, _, _, _ = build(pkg, w, dev, seed=3)
+    lin = dec.decoder[-1]
+
+    def fused_step():
+        nll, reg = loss_head.fused_loss_head(ode, lat, lin, y, S, B)
+        (nll + 0.1 * reg).backward()
+
+    def ref_step():
+        yp = dec(lat[..., :3]).reshape((-1, S, B, R)).permute(2, 1, 0, 3)
+        (tf.nll_loss(yp, y) + 0.1 * tf.latent_init_loss(lat[..., :3])).backward()
+
+    def run(fn, ev):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        fused.EVENTS = [] if ev else None
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / reps
+        evs, fused.EVENTS = fused.EVENTS, None
+        k = {}
+        for kind, e0, e1 in evs or []:
+            k.setdefault(kind, []).append(e0.elapsed_time(e1))
+        return el, {kk: sum(v) / len(v) for kk, v in k.items()}
+
+    el_f, k = run(fused_step, True)
+    el_r, _ = run(ref_step, False)
+    lat_bytes = lat.numel() * 4
+    fwd_gbs = lat_bytes / (k["loss_fwd"] * 1e-3) / 1e9
+    bwd_gbs = 2 * lat_bytes / (k["loss_bwd"] * 1e-3) / 1e9
+    return {"workload": f"state49 latent (T={T}, S={S}, B={B}, R={R}, L={L}) -> Decoder + nll_loss + "
+                        "latent_init_loss, fwd+bwd",
+            "fused_ms_per_step": el_f * 1e3, "reference_torch_gpu_ms_per_step": el_r * 1e3,
+            "speedup_vs_reference_ops": el_r / el_f,
+            "fwd_kernel_ms": k["loss_fwd"], "bwd_kernel_ms": k["loss_bwd"],
+            "roofline": {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                         "fwd_achieved": fwd_gbs, "fwd_frac": fwd_gbs / PEAK_HBM_GBS,
+                         "bwd_achieved": bwd_gbs, "bwd_frac": bwd_gbs / PEAK_HBM_GBS,
+                         "algorithmic_bytes": {"fwd": lat_bytes, "bwd": 2 * lat_bytes}}}
+
+
 def _cpu_copy(mod):
     import copy
     mod.clear_tracking()
@@ -308,6 +365,7 @@ def main():
         del m3, y3, d3
     if rank == 0 and world == 1 and not args.no_extra and args.workload == "state49":
         res["dopri5_state49"] = dopri5_line(pkg, w, dev)
+        res["loss_head_state49"] = loss_head_line(pkg, w, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(w, mod)
     if rank == 0:

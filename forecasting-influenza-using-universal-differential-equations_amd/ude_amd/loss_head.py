@@ -29,8 +29,12 @@ class _LossHead(torch.autograd.Function):
         ws = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=dev)
         out = torch.empty(2, dtype=torch.float32, device=dev)
         latent, W, b, y = latent.contiguous(), W.contiguous(), b.contiguous(), y.contiguous()
+        if _fused.EVENTS is not None:
+            e0 = _fused._ev(dev); e0.record()
         lib.loss_forward(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(), ws.data_ptr(),
                          out.data_ptr(), stream)
+        if _fused.EVENTS is not None:
+            e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_fwd", e0, e1))
         ctx.meta = (lib, desc, T, S, B)
         ctx.save_for_backward(latent, W, b, y, ws)
         return out[0], out[1]
@@ -46,9 +50,13 @@ class _LossHead(torch.autograd.Function):
         dlat = torch.empty_like(latent)
         dW = torch.empty_like(W)
         db = torch.empty_like(b)
+        if _fused.EVENTS is not None:
+            e0 = _fused._ev(dev); e0.record()
         lib.loss_backward(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
                           grad.data_ptr(), ws.data_ptr(), dlat.data_ptr(), dW.data_ptr(), db.data_ptr(),
                           _fused._stream(dev))
+        if _fused.EVENTS is not None:
+            e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_bwd", e0, e1))
         return None, None, None, None, None, dlat, dW, db, None
 
 

@@ -37,17 +37,27 @@ METRIC = "UDE trajectories×steps/sec (fwd+bwd), batch=states×seasons, at 1/2/4
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector == FP32 MFMA dense peak
 PEAK_HBM_GBS = 8000.0
 
+_US = dict(kind="FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64])
+_STATE = dict(kind="FaFp", R=49, L=8, net=[64, 64, 32], aug=[64, 64])
 WORKLOADS = {
-    "state49": dict(kind="FaFp", R=49, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=64 * 10 * 32,
-                    t=("arange", 9, 1.0),
+    "state49": dict(_STATE, n_traj=64 * 10 * 32, t=("arange", 9, 1.0),
                     desc="state model R=49 (joint), 64 MC samples x 10 seasons x 32 windows, 8 weekly RK4 steps"),
-    "us_northstar": dict(kind="FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=4096,
-                         t=("arange", 366, 7.0),
+    "state49_n2048": dict(_STATE, n_traj=2048, t=("arange", 9, 1.0),
+                          desc="state model R=49 (joint), the reference's own batch: 64 MC samples x 32 windows, "
+                               "8 weekly RK4 steps (SURVEY 8d M2 variant)"),
+    "m3_states_r1": dict(_US, n_traj=64 * 50 * 10 * 32, t=("arange", 9, 1.0),
+                         desc="50 independent states as R=1 US-architecture models: 64 samples x 50 states x "
+                              "10 seasons x 32 windows = 1,024,000 trajectories, 8 weekly RK4 steps (SURVEY 8d M3)"),
+    "us_northstar": dict(_US, n_traj=4096, t=("arange", 366, 7.0),
                          desc="US model R=1, 4096 trajectories x 365 daily RK4 steps (north-star M1)"),
-    "bayes_us": dict(kind="Bayes_FaFp", R=1, L=8, net=[64, 64, 32], aug=[64, 64], n_traj=4096,
-                     t=("arange", 366, 7.0),
+    "us_fp32": dict(kind="Fp", R=1, L=8, net=[32, 32], aug=None, n_traj=4096, t=("arange", 366, 7.0),
+                    desc="US Fp [32, 32] ('32-hidden' north-star model), R=1, 4096 trajectories x 365 daily "
+                         "RK4 steps (north-star M1)"),
+    "bayes_us": dict(_US, kind="Bayes_FaFp", n_traj=4096, t=("arange", 366, 7.0),
                      desc="Bayesian US model (models_bayes.py Bayes_FaFp, fresh weight sample per RHS "
                           "evaluation), R=1, 4096 trajectories x 365 daily RK4 steps"),
+    "tiny": dict(_US, n_traj=64, t=("arange", 5, 1.0),
+                 desc="plumbing rehearsal only (CPU / gloo): US model, 64 trajectories, 4 weekly steps"),
 }
 
 
@@ -126,21 +136,21 @@ def one_step(pkg, udist, mod, y0, t, dlat, world):
         udist.all_reduce_grads(mod.parameters())
 
 
-def time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier):
+def time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier, dev):
     from ude_amd import fused
     for _ in range(warmup):
         one_step(pkg, udist, mod, y0, t, dlat, world)
-    torch.cuda.synchronize()
-    fused.EVENTS = []
+    _sync(dev)
+    fused.EVENTS = [] if dev.type == "cuda" else None
     barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         one_step(pkg, udist, mod, y0, t, dlat, world)
     barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     el = time.perf_counter() - t0
-    evs = fused.EVENTS
+    evs = fused.EVENTS or []
     fused.EVENTS = None
     k_ms = {"fwd": [], "bwd": []}
     for kind, e0, e1 in evs:
@@ -148,10 +158,15 @@ def time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier):
     return el, {k: (sum(v) / len(v) if v else None) for k, v in k_ms.items()}
 
 
-def cpu_baseline(w, mod_gpu, budget_s=12.0):
+# host threads of the CPU baseline: the GPU box's CPU share per GPU (OMP_NUM_THREADS there)
+CPU_THREADS = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+
+
+def cpu_baseline(w, mod_gpu, budget_s=10.0, threads=1):
     """The oracle (PyTorch CPU restatement, fp32, autograd) on a bounded sample."""
     from oracle.ude_oracle import OracleRHS, solve_and_grad
-    torch.set_num_threads(1)                     # the reference's own setting (run_ode.py:28)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)              # 1 = the reference's own setting (run_ode.py:28)
     rhs = OracleRHS.from_module(_cpu_copy(mod_gpu))
     n = 1024 if w["R"] > 10 else 4096
     steps_cap = 8 if w["R"] > 10 else 40
@@ -169,12 +184,13 @@ def cpu_baseline(w, mod_gpu, budget_s=12.0):
         d = time.perf_counter() - a
         best = d if best is None else min(best, d)
         reps += 1
+    torch.set_num_threads(prev)
     units = n * (len(tt) - 1)
-    return {"value": units / best, "unit": "traj*steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/ude_oracle.py (PyTorch CPU fp32 + autograd, torch.set_num_threads(1) as "
-                      f"run_ode.py:28) on {n} trajectories x {len(tt) - 1} steps of the same model, "
-                      f"fwd+bwd incl. posterior/|Fa| terms, best of {reps}",
-            "host_cpus": os.cpu_count()}
+    return {"value": units / best, "unit": "traj*steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ude_oracle.py (PyTorch CPU fp32 + autograd, torch.set_num_threads({threads}); "
+                      f"the reference runs 1 thread, run_ode.py:28) on {n} trajectories x {len(tt) - 1} steps of "
+                      f"the same model, fwd+bwd incl. posterior/|Fa| terms, best of {reps}",
+            "host_cpus_visible": os.cpu_count()}
 
 
 def dopri5_line(pkg, w, dev, reps=3):
@@ -277,29 +293,99 @@ def read_pmc(name):
         return None
 
 
+def _launch_workers(n):
+    """`bench.py --gpus N` run without a launcher: start N ranks under torch.distributed.run
+    as a child process (before this process touches the GPU) and exit with its code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, UDE_BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def measure(pkg, udist, w, n_traj, dev, rank, world, steps, warmup, barrier):
+    """Time `steps` fwd+bwd steps of workload w with n_traj trajectories on this rank;
+    returns (max-over-ranks seconds, HIP-event kernel averages)."""
+    import torch.distributed as dist
+    w = dict(w, n_traj=n_traj)
+    mod, y0, t, dlat = build(pkg, w, dev, seed=1000 + rank)
+    el, kms = time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier, dev)
+    if world > 1:
+        x = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x)
+    return el, kms, mod, len(t) - 1
+
+
+def extra_line(pkg, udist, name, dev, barrier, steps=3):
+    w = WORKLOADS[name]
+    m, y, t, d = build(pkg, w, dev, seed=7)
+    el, k = time_steps(pkg, udist, m, y, t, d, 1, steps, 1, barrier, dev)
+    n_rk = len(t) - 1
+    v = w["n_traj"] * n_rk * steps / el
+    macs = macs_per_eval(w)
+    out = {"workload": name, "description": w["desc"], "traj_steps_per_s": v, "rhs_evals_per_s": 4 * v,
+           "ms_per_step": el / steps * 1e3, "fwd_ms": k["fwd"], "bwd_ms": k["bwd"]}
+    if k["bwd"] and not w["kind"].startswith("Bayes_"):
+        bwd_flop = 4 * 4 * macs * w["n_traj"] * n_rk
+        fwd_flop = 4 * 2 * macs * w["n_traj"] * n_rk
+        out["bwd_tflops"] = bwd_flop / (k["bwd"] * 1e-3) / 1e12
+        out["bwd_frac"] = out["bwd_tflops"] / PEAK_FP32_TFLOPS
+        out["fwd_tflops"] = fwd_flop / (k["fwd"] * 1e-3) / 1e12
+        out["fwd_frac"] = out["fwd_tflops"] / PEAK_FP32_TFLOPS
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="state49", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: every rank solves the workload's batch; strong: the batch is split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo only to rehearse N>1")
+    ap.add_argument("--rehearse-cpu", action="store_true",
+                    help="plumbing rehearsal on the host (gloo, eager solver): checks ranks / batch accounting")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(_launch_workers(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a mislabelled number",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch.distributed as dist
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % max(ndev, 1))
-    torch.cuda.set_device(dev)
+    if args.rehearse_cpu:
+        dev = torch.device("cpu")
+        backend = "gloo"
+    else:
+        ndev = torch.cuda.device_count()
+        dev = torch.device("cuda", local % max(ndev, 1))
+        torch.cuda.set_device(dev)
+        backend = args.dist_backend
     if world > 1:
-        if args.dist_backend == "nccl":
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(backend)
+        world = dist.get_world_size()                 # n_gpus comes from the process group
+        rank = dist.get_rank()
         barrier = lambda: dist.barrier()
     else:
         barrier = lambda: None
@@ -308,19 +394,25 @@ def main():
     from ude_amd import distributed as udist
 
     w = WORKLOADS[args.workload]
-    mod, y0, t, dlat = build(pkg, w, dev, seed=1000 + rank)
-    el, kms = time_steps(pkg, udist, mod, y0, t, dlat, world, args.steps, args.warmup, barrier)
-    if world > 1:
-        x = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        el = float(x)
-    n_steps_rk = len(t) - 1
-    units = world * w["n_traj"] * n_steps_rk * args.steps
+    per_rank = w["n_traj"] if args.scaling == "weak" else w["n_traj"] // world
+    if args.scaling == "strong" and per_rank * world != w["n_traj"]:
+        raise SystemExit(f"strong scaling: {w['n_traj']} trajectories do not split over {world} ranks")
+    el, kms, mod, n_steps_rk = measure(pkg, udist, w, per_rank, dev, rank, world, args.steps, args.warmup, barrier)
+    units = world * per_rank * n_steps_rk * args.steps
     value = units / el
     macs = macs_per_eval(w)
     flop_unit = 4 * 6 * macs                                  # fwd + dX + dW per traj*step
-    bwd_flop_launch = 4 * 4 * macs * w["n_traj"] * n_steps_rk  # dX + dW only (recompute not counted)
-    fwd_flop_launch = 4 * 2 * macs * w["n_traj"] * n_steps_rk
+    bwd_flop_launch = 4 * 4 * macs * per_rank * n_steps_rk    # dX + dW only (recompute not counted)
+    fwd_flop_launch = 4 * 2 * macs * per_rank * n_steps_rk
+
+    # strong-scaling companion (N > 1, weak headline): the same global batch split over the ranks
+    strong = None
+    if world > 1 and args.scaling == "weak" and not args.no_extra and w["n_traj"] % world == 0:
+        el_s, kms_s, _, _ = measure(pkg, udist, w, w["n_traj"] // world, dev, rank, world, args.steps,
+                                    args.warmup, barrier)
+        strong = {"scaling": "strong", "global_batch": w["n_traj"], "traj_per_gpu": w["n_traj"] // world,
+                  "value": w["n_traj"] * n_steps_rk * args.steps / el_s, "unit": "traj*steps/s",
+                  "ms_per_step": el_s / args.steps * 1e3, "bwd_ms": kms_s["bwd"]}
 
     res = None
     if rank == 0:
@@ -329,12 +421,13 @@ def main():
         res = {
             "metric": METRIC, "value": value, "unit": "traj*steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded y0 per SURVEY 8d, default nn.Linear init, N(0,1) d latent)",
             "config": {"workload": args.workload, "description": w["desc"], "model": w["kind"],
                        "n_regions": w["R"], "latent_dim": w["L"], "net_sizes": w["net"],
-                       "aug_net_sizes": w["aug"], "traj_per_gpu": w["n_traj"], "global_batch": world * w["n_traj"],
-                       "rk4_steps": n_steps_rk, "parallelism": f"dp{world}"},
+                       "aug_net_sizes": w["aug"], "traj_per_gpu": per_rank, "global_batch": world * per_rank,
+                       "rk4_steps": n_steps_rk, "parallelism": f"dp{world}",
+                       "device": "cpu-rehearsal" if args.rehearse_cpu else "MI355X"},
             "roofline": {"kernel": "ude_bwd_kernel (+ grad finalize)", "bound": "mfma",
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
@@ -345,29 +438,20 @@ def main():
                         "step_tflops_algorithmic": value * flop_unit / 1e12,
                         "rhs_evals_per_s": 4 * value},
         }
-    if rank == 0 and world == 1 and not args.no_extra and args.workload == "state49":
-        w2 = WORKLOADS["us_northstar"]
-        m2, y2, t2, d2 = build(pkg, w2, dev, seed=7)
-        el2, k2 = time_steps(pkg, udist, m2, y2, t2, d2, 1, 3, 1, barrier)
-        v2 = w2["n_traj"] * (len(t2) - 1) * 3 / el2
-        res["north_star_M1"] = {"workload": "us_northstar", "description": w2["desc"],
-                                "traj_steps_per_s": v2, "rhs_evals_per_s": 4 * v2,
-                                "ms_per_step": el2 / 3 * 1e3, "fwd_ms": k2["fwd"], "bwd_ms": k2["bwd"],
-                                "target_rhs_evals_per_s": 1e7}
-        del m2, y2, d2
-        w3 = WORKLOADS["bayes_us"]
-        m3, y3, t3, d3 = build(pkg, w3, dev, seed=9)
-        el3, k3 = time_steps(pkg, udist, m3, y3, t3, d3, 1, 3, 1, barrier)
-        v3 = w3["n_traj"] * (len(t3) - 1) * 3 / el3
-        res["bayes_M1"] = {"workload": "bayes_us", "description": w3["desc"], "traj_steps_per_s": v3,
-                           "rhs_evals_per_s": 4 * v3, "ms_per_step": el3 / 3 * 1e3, "fwd_ms": k3["fwd"],
-                           "bwd_ms": k3["bwd"]}
-        del m3, y3, d3
-    if rank == 0 and world == 1 and not args.no_extra and args.workload == "state49":
+        if strong is not None:
+            res["strong_scaling"] = strong
+    extra = rank == 0 and world == 1 and not args.no_extra and args.workload == "state49" and not args.rehearse_cpu
+    if extra:
+        res["north_star_M1"] = dict(extra_line(pkg, udist, "us_northstar", dev, barrier), target_rhs_evals_per_s=1e7)
+        res["north_star_M1_fp32"] = extra_line(pkg, udist, "us_fp32", dev, barrier)
+        res["M2_state49_n2048"] = extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=10)
+        res["M3_states_r1"] = extra_line(pkg, udist, "m3_states_r1", dev, barrier)
+        res["bayes_M1"] = extra_line(pkg, udist, "bayes_us", dev, barrier)
         res["dopri5_state49"] = dopri5_line(pkg, w, dev)
         res["loss_head_state49"] = loss_head_line(pkg, w, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(w, mod)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.rehearse_cpu:
+        res["cpu_baseline"] = cpu_baseline(w, mod, threads=CPU_THREADS)
+        res["cpu_baseline_1thread"] = cpu_baseline(w, mod, threads=1)
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

@@ -33,12 +33,18 @@ bool matches(const UdeModelDesc* d) {
 
 template <class M>
 struct Ops {
+  static constexpr int DY0_STATIC_LDS = TT * M::R * M::L * 4;
+  static_assert(!M::HOIST || DY0_STATIC_LDS <= 160 * 1024, "dy0 static time sums do not fit the 160 KiB LDS");
   static int ensure_attrs() {
     static bool done = false;
     if (done) return UDE_OK;
     HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
     HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
     HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_B));
+    // the static-feature dy0 kernel stages one tile's (16, R, L) time sums of d latent in LDS
+    if (M::HOIST)
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 DY0_STATIC_LDS));
     done = true;
     return UDE_OK;
   }

@@ -133,7 +133,21 @@ class VAE:
             return None
         if not loss_head.eligible(self.ode, self.latent, lin, src[1], src[2]):
             return None
-        return loss_head.fused_loss_head(self.ode, self.latent, lin, y_true, src[1], src[2])
+        return loss_head.fused_loss_head(self.ode, self.latent, lin, y_true, src[1], src[2], group_stats=True)
+
+    @staticmethod
+    def _validate_normals(checks):
+        """The Normal argument checks the reference's nll_loss / posterior() get from
+        torch.distributions (scale > 0, finite loc), for parameters that live on a HIP device:
+        one batched read-back (calc_loss reads its loss terms back anyway) instead of one per
+        Normal; raises ValueError as torch's validation does."""
+        if not checks:
+            return
+        flags = torch.stack([((~(scale > 0)).any() | (loc != loc).any()) for _, loc, scale in checks]).cpu()
+        for (what, loc, scale), bad in zip(checks, flags.tolist()):
+            if bad:
+                raise ValueError(f"Expected parameters loc / scale of distribution Normal ({what}) to satisfy the "
+                                 "constraints Real() / GreaterThan(lower_bound=0.0), but found invalid values")
 
     def calc_loss(self, y_pred, y_true, losses):
         terms = {}
@@ -143,6 +157,9 @@ class VAE:
         if losses.get("mse", True):
             terms["mse"] = torch.mean(torch.square(y_pred - y_true.unsqueeze(1)))
         fused = self._fused_head(y_pred, y_true, losses)
+        checks = []
+        if fused is not None:
+            checks.append(("nll_loss prediction mean / std", fused[2][..., 0], fused[2][..., 1]))
         if losses.get("nll", True):
             terms["nll"] = fused[0] if fused is not None else train_functions.nll_loss(y_pred, y_true)
         if losses.get("kl_z", True):
@@ -150,8 +167,11 @@ class VAE:
             kl = train_functions.kl_divergence(prior, Normal(self.mean, self.std)).sum(-1).mean()
             terms["kl_latent"] = self.kl_w * kl / self.len_tr
         if losses.get("kl_p", True):
+            post = self.ode.posterior()
+            if post.loc.is_cuda:
+                checks.append(("ode.posterior()", post.loc, post.scale))
             terms["kl_params"] = train_functions.get_kl_params(
-                1, self.ode.posterior(), means=self.prior_params["means"], stds=self.prior_params["stds"],
+                1, post, means=self.prior_params["means"], stds=self.prior_params["stds"],
                 limit=1e6, device=self.device)
         norm = None
         if losses.get("Fa_norm", 0) > 0:
@@ -162,6 +182,7 @@ class VAE:
                                        else train_functions.latent_init_loss(self.latent[..., :3]))
         if self.ode.uncertainty == "bayes":
             terms["ode_kl"] = self.ode_kl_w * self.ode.get_kl()
+        self._validate_normals(checks)
         loss = torch.tensor(0.0, requires_grad=True)
         for v in terms.values():
             loss = loss + v

@@ -61,20 +61,34 @@ def sync_side_stats(module) -> None:
     """Replace the module's recorded fused-solve statistics by their global values."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return
-    rates = list(module._fused_rates)
+    # eager evaluations (params / tracker lists of per-evaluation tensors) are folded into
+    # the same sufficient statistics as the fused solves' entries
+    groups = list(module._fused_rates)
+    if module.params:
+        p = torch.stack(module.params).reshape(-1, 2)
+        groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
     tracker = list(module.tracker)
-    if not rates and not tracker:
+    if not groups and not tracker:
         return
-    if rates:
-        n, m, s = rates[-1]
+    if groups:
+        n = sum(g[0] for g in groups)
+        m = sum(g[0] * g[1] for g in groups) / n
+        s = torch.sqrt(sum((g[0] - 1.0) * g[2] ** 2 + g[0] * (g[1] - m) ** 2 for g in groups) / (n - 1.0)) \
+            if len(groups) > 1 else groups[0][2]
     else:
-        n, m, s = 1.0, torch.zeros(2, device=tracker[-1].device), torch.ones(2, device=tracker[-1].device)
-    norm = tracker[-1] if tracker else torch.zeros(1, device=m.device)
-    n_tot, gm, gs, gn = combine_stats(n, m, s, norm)
-    if rates:
-        module._fused_rates[-1] = (n_tot, gm, gs)
+        dev = tracker[-1].device
+        n, m, s = 1.0, torch.zeros(2, device=dev), torch.ones(2, device=dev)
+    # == torch.norm(torch.stack(tracker)) of lib/VAE.py:180 (the norm of every entry together)
     if tracker:
-        module.tracker[-1] = gn
+        norm = torch.norm(torch.cat([x.reshape(-1) for x in tracker])).reshape(1)
+    else:
+        norm = torch.zeros(1, device=m.device)
+    n_tot, gm, gs, gn = combine_stats(n, m, s, norm)
+    module.params = []
+    if groups:
+        module._fused_rates = [(n_tot.detach(), gm, gs)]
+    if tracker:
+        module.tracker = [gn]
 
 
 def all_reduce_grads(params: Iterable[torch.nn.Parameter], average: bool = True) -> None:

@@ -37,12 +37,19 @@ class _LossHead(torch.autograd.Function):
             e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_fwd", e0, e1))
         ctx.meta = (lib, desc, T, S, B)
         ctx.save_for_backward(latent, W, b, y, ws)
-        return out[0], out[1]
+        ctx.mark_non_differentiable(ws)
+        # ws starts with the per-(t, b, r) sample mean / std of the predictions ((T, B, R, 2))
+        return out[0], out[1], ws
 
     @staticmethod
-    def backward(ctx, g_nll, g_reg):
+    def backward(ctx, g_nll, g_reg, _g_ws=None):
         lib, desc, T, S, B = ctx.meta
         latent, W, b, y, ws = ctx.saved_tensors
+        with torch.cuda.device(latent.device):
+            return _LossHead._backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg)
+
+    @staticmethod
+    def _backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg):
         dev = latent.device
         zero = torch.zeros((), dtype=torch.float32, device=dev)
         grad = torch.stack([zero if g_nll is None else g_nll.float().reshape(()),
@@ -60,22 +67,53 @@ class _LossHead(torch.autograd.Function):
         return None, None, None, None, None, dlat, dW, db, None
 
 
+_FITS = {}
+
+
+def _fits(cfg, T: int, S: int, B: int, device: torch.device) -> bool:
+    """Whether the kernel takes (T, S, B): the sample count bounds its per-group register /
+    LDS tiles (pad16(S) <= 128, LDS <= 160 KiB), which ude_loss_head_workspace checks."""
+    key = (cfg, T, S, B, str(device))
+    hit = _FITS.get(key)
+    if hit is None:
+        try:
+            lib = _native.library_for(cfg)
+            dev_index = device.index if device.index is not None else torch.cuda.current_device()
+            lib.loss_workspace(_native.make_desc(cfg), T, S, B, dev_index)
+            hit = True
+        except _native.UdeError:
+            hit = False
+        _FITS[key] = hit
+    return hit
+
+
 def eligible(ode, latent: torch.Tensor, linear, n_samples: int, batch: int) -> bool:
     R = ode.n_regions
-    return (latent.is_cuda and latent.dtype == torch.float32 and latent.dim() == 4 and n_samples >= 2
-            and latent.shape[1] == n_samples * batch and latent.shape[2] == R and latent.shape[3] >= 3
+    if not (latent.is_cuda and latent.dtype == torch.float32 and latent.dim() == 4 and n_samples >= 2
+            and latent.shape[1] == n_samples * batch and latent.shape[2] == R
+            and latent.shape[3] == ode.latent_dim and latent.is_contiguous() and latent.data_ptr() % 16 == 0
             and isinstance(linear, torch.nn.Linear) and tuple(linear.weight.shape) == (R, 3 * R)
-            and linear.bias is not None and linear.weight.dtype == torch.float32 and linear.weight.is_cuda
-            and _native.config_supported(ode.ude_config()))
+            and linear.bias is not None and linear.weight.dtype == torch.float32
+            and linear.weight.device == latent.device
+            and _native.config_supported(ode.ude_config())):
+        return False
+    return _fits(ode.ude_config(), int(latent.shape[0]), int(n_samples), int(batch), latent.device)
 
 
 def fused_loss_head(ode, latent: torch.Tensor, linear: torch.nn.Linear, y: torch.Tensor, n_samples: int,
-                    batch: int):
+                    batch: int, group_stats: bool = False):
+    """(nll, reg); with group_stats=True also the (T, B, R, 2) per-group prediction mean / std
+    (the Normal parameters nll_loss builds, for the caller's argument validation)."""
     cfg = ode.ude_config()
     lib = _native.library_for(cfg)
     desc = _native.make_desc(cfg)
     T = int(latent.shape[0])
     if tuple(y.shape) != (batch, T, ode.n_regions):
         raise ValueError(f"targets {tuple(y.shape)} do not match (B, T, R) = {(batch, T, ode.n_regions)}")
-    return _LossHead.apply(lib, desc, T, int(n_samples), int(batch), latent, linear.weight, linear.bias,
-                           y.to(torch.float32))
+    with torch.cuda.device(latent.device):
+        nll, reg, ws = _LossHead.apply(lib, desc, T, int(n_samples), int(batch), latent, linear.weight,
+                                       linear.bias, y.to(torch.float32))
+    if group_stats:
+        R = ode.n_regions
+        return nll, reg, ws.view(torch.float32)[: T * batch * R * 2].view(T, batch, R, 2)
+    return nll, reg

@@ -35,7 +35,7 @@ def load_golden(name):
 
 def solver_cases():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("rhs_", "e2e_", "bayes_")))
+                  if not os.path.basename(p).startswith(("rhs_", "e2e_", "bayes_", "loss_")))
 
 
 def bayes_cases():

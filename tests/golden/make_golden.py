@@ -234,7 +234,107 @@ def make_e2e():
     print("e2e fixture written, loss", float(loss), dict(zip(names, data)))
 
 
+def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, seed):
+    """End-to-end training step of the reference VAE at a given region count, run twice by the
+    reference code itself: in fp32 (the reference's dtype) and in fp64 (the parity target; the
+    fp32-vs-fp64 distance of the reference's own step sets the tolerance).  The eps draw of
+    VAE.__call__ is pinned by replacing torch.randn for the duration of the call."""
+    import copy
+    import types
+    td = types.ModuleType("torchdiffeq")
+
+    def _odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None):
+        assert method == "rk4"
+        return odeint_rk4(func, y0, t, (options or {}).get("step_size"))
+    td.odeint = _odeint
+    sys.modules["torchdiffeq"] = td
+    import lib.VAE as ref_vae
+    torch.manual_seed(seed)
+    model = ref_vae.VAE(ref_models.Encoder_Back_GRU, ref_models.FaFp, ref_models.Decoder, n_qs, 8, R,
+                        ode_params=dict(ode_params, prior_std=0.05), enc_params=enc_params,
+                        uncertainty=True, ode_kl_w=1 / 153)
+    gen = torch.Generator().manual_seed(seed + 1)
+    x = torch.rand(B, window, R * (n_qs + 1), generator=gen)
+    t = torch.arange(window + gamma + 1, dtype=torch.float32) / 7
+    eval_pts = np.arange(0, gamma + 1, 7)                # run_ode.py's longest curriculum stage
+    y = torch.rand(B, len(t), R, generator=gen) * 0.5
+    y[0, 7, 0] = -1.0                                    # masked targets (train_functions.nll_loss)
+    y[-1, 14, R - 1] = -1.0
+    eps = torch.randn(S_, B, R, model.ld_enc, generator=gen)
+    losses = {"nll": True, "mse": False, "kl_z": True, "kl_p": True, "Fa_norm": 1e-1, "reg_loss": True,
+              "anneal": True}
+    sd = {part: {k: v.clone() for k, v in getattr(model, part).state_dict().items()}
+          for part in ("enc", "ode", "dec")}
+
+    def step(dtype):
+        m = copy.deepcopy(model)
+        for part in ("enc", "ode", "dec"):
+            getattr(m, part).to(dtype)
+        m.dtype = dtype
+        m.enc.scaler = m.enc.scaler.to(dtype)
+        m.setup_training(lr=1e-3)
+        real_randn = torch.randn
+        torch.randn = lambda *a, **k: eps.to(dtype).clone()
+        try:
+            y_pred = m(x.to(dtype), t[eval_pts].to(dtype), n_samples=S_, training=True)
+        finally:
+            torch.randn = real_randn
+        loss, data, names = m.calc_loss(y_pred, y[:, eval_pts, :].to(dtype), losses)
+        loss.backward()
+        out = {"loss": loss.detach().reshape(1), "y_pred": y_pred.detach(), "latent": m.latent.detach()}
+        for part in ("enc", "ode", "dec"):
+            for k, p in getattr(m, part).named_parameters():
+                out[f"g_{part}.{k}"] = p.grad.detach()
+        return out, names, data
+
+    o32, names, data = step(torch.float32)
+    o64, _, _ = step(torch.float64)
+    arrs = {"x": x.numpy(), "y": y.numpy(), "t": t.numpy(), "eval_pts": eval_pts, "eps": eps.numpy()}
+    for part in ("enc", "ode", "dec"):
+        for k, v in sd[part].items():
+            arrs[f"w_{part}.{k}"] = v.numpy()
+    for k, v in o64.items():
+        # the (T, N, R, L) latent is kept at fp32 precision (6e-8 rounding, far under every bar)
+        arrs["ref64_" + k] = v.float().numpy() if k == "latent" else v.numpy()
+    arrs["ref32_loss"] = o32["loss"].numpy()
+    dist = {k: normwise_rel(o32[k], o64[k]) for k in o64}
+    meta = {"B": B, "window": window, "gamma": gamma, "n_qs": n_qs, "n_regions": R, "n_samples": S_,
+            "losses": losses, "loss_names": names, "loss_data": data, "ode_params": ode_params,
+            "enc_params": enc_params, "ref32_vs_ref64": dist,
+            "generator": "tests/golden/make_golden.py make_e2e_case (reference lib/VAE.py + lib/models.py, "
+                         "oracle RK4 as torchdiffeq), fp32 and fp64 runs of the reference step"}
+    arrs["meta_json"] = np.array(json.dumps(meta))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+    print(f"{name}: loss32 {float(o32['loss'])} loss64 {float(o64['loss'])}, worst ref32-vs-ref64 "
+          f"{max(dist.values()):.2e}", dict(zip(names, data)))
+
+
+def make_e2e_state49():
+    # configs[3]: the reference's state model (run_ode.py:41-49: R = 49, L = 8, FaFp net [64, 64, 32],
+    # aug [64, 64], n_qs 8), 64 MC samples (run_ode.py:37), 9 weekly outputs (gamma 56); the GRU
+    # encoder (out of scope, plain PyTorch) is narrowed to keep the fixture small
+    make_e2e_case("e2e_vae_state49", R=49, n_qs=8, B=2, S_=64, window=8, gamma=56,
+                  ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
+                  enc_params={"q_sizes": [32, 16], "ff_sizes": [16, 16], "SIR_scaler": [0.1, 0.05, 1.0]},
+                  seed=4949)
+
+
+def make_e2e_us():
+    # the reference's US model (run_ode.py:59-66: R = 1, L = 8, FaFp [64, 64, 32] / [64, 64]) at
+    # run_ode.py's training batch shape (64 MC samples), narrowed encoder as above
+    make_e2e_case("e2e_vae_us", R=1, n_qs=90, B=8, S_=64, window=8, gamma=56,
+                  ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
+                  enc_params={"q_sizes": [32, 16], "ff_sizes": [16, 16], "SIR_scaler": [0.1, 0.05, 1.0]},
+                  seed=1111)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) == 1:
-        main()
-    make_e2e()
+    torch.set_num_threads(1)
+    if len(sys.argv) > 1 and sys.argv[1] == "e2e_state49":
+        make_e2e_state49()
+    elif len(sys.argv) > 1 and sys.argv[1] == "e2e_us":
+        make_e2e_us()
+    else:
+        if len(sys.argv) == 1:
+            main()
+        make_e2e()

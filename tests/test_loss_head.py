@@ -1,53 +1,47 @@
 """Fused loss head (csrc/ude_loss.h): decoder + nll_loss + latent_init_loss, forward and
-backward, against the same terms computed with the reference's formulas in fp64
-(lib/models.py:27-51 Decoder, lib/VAE.py:138 reshape/permute,
-lib/train_functions.py:81-90 nll_loss, :116-126 latent_init_loss).
+backward, against fixtures made by the reference's own code in fp64
+(tests/golden/make_golden_loss.py: lib/models.py:27-51 Decoder, lib/VAE.py:138 reshape /
+permute, lib/train_functions.py:81-90 nll_loss, :116-126 latent_init_loss).
 
 Tolerance: normwise relative 1e-5 for the loss values and the gradients (fp32 kernel vs
-fp64 reference; the sample mean / std are fp32 sums over S <= 64 terms)."""
+fp64 reference; the sample mean / std are fp32 sums over S <= 128 terms).  Cases include
+S = 128 (the kernel's largest sample tile, ~157 KiB of LDS at R = 49) and ragged S."""
+import os
+import sys
+
+import numpy as np
 import pytest
 import torch
 
+from conftest import GOLDEN, load_golden
 from helpers import normwise_rel
+
+sys.path.insert(0, GOLDEN)
+import make_golden_loss as mgl  # noqa: E402  (input recipe only; runs no reference code)
 
 DEV = "cuda"
 
 
-def _reference(latent, W, b, y, S, B, g_nll, g_reg):
-    import lib.train_functions as tf
-    lat = latent.detach().double().requires_grad_(True)
-    Wd = W.detach().double().requires_grad_(True)
-    bd = b.detach().double().requires_grad_(True)
-    T, N, R, L = lat.shape
-    x = lat[..., :3]
-    dec = torch.nn.functional.linear(x.reshape(-1, R * 3), Wd, bd).reshape(T, N, R)
-    y_pred = dec.reshape((-1, S, B, R)).permute(2, 1, 0, 3)
-    nll = tf.nll_loss(y_pred, y.double())
-    reg = tf.latent_init_loss(x)
-    (g_nll * nll + g_reg * reg).backward()
-    return nll.detach(), reg.detach(), lat.grad, Wd.grad, bd.grad
+def test_loss_fixture_inputs_regenerate():
+    """The seeded input recipe reproduces the inputs the fixtures were made from."""
+    for case in mgl.CASES:
+        g = load_golden(mgl.case_name(case))
+        assert np.allclose(mgl.checksum(*mgl.inputs(case)), g["meta"]["checksum"], rtol=0, atol=0)
 
 
-CASES = [  # R, L, T, S, B
-    (1, 8, 9, 64, 32), (10, 8, 5, 64, 8), (49, 8, 3, 64, 6), (1, 8, 4, 5, 4), (3, 5, 6, 17, 3),
-]
+def _ode_for(pkg, R, L):
+    net, aug = ([40, 24], [36]) if R == 3 else ([64, 64, 32], [64, 64])     # prebuilt configurations
+    return pkg.FaFp(R, latent_dim=L, net_sizes=net, aug_net_sizes=aug).to(DEV)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "R{}_L{}_T{}_S{}_B{}".format(*c))
+@pytest.mark.parametrize("case", mgl.CASES, ids=mgl.case_name)
 def test_fused_loss_head_matches_reference(pkg, case):
     from ude_amd import loss_head
     R, L, T, S, B = case
-    torch.manual_seed(R * 100 + S)
-    net, aug = ([40, 24], [36]) if R == 3 else ([64, 64, 32], [64, 64])     # prebuilt configurations
-    ode = pkg.FaFp(R, latent_dim=L, net_sizes=net, aug_net_sizes=aug).to(DEV)
-    gen = torch.Generator().manual_seed(7)
-    latent = (torch.rand(T, S * B, R, L, generator=gen) * 2.0 - 0.5)
-    W = torch.randn(R, 3 * R, generator=gen) * 0.3
-    b = torch.randn(R, generator=gen) * 0.1
-    y = torch.rand(B, T, R, generator=gen)
-    y[0, 0, 0] = -1.0
-    y[-1, -1, -1] = -1.0
+    g = load_golden(mgl.case_name(case))
+    latent, W, b, y = mgl.inputs(case)
+    ode = _ode_for(pkg, R, L)
     lin = torch.nn.Linear(3 * R, R).to(DEV)
     with torch.no_grad():
         lin.weight.copy_(W)
@@ -55,10 +49,72 @@ def test_fused_loss_head_matches_reference(pkg, case):
     lat = latent.to(DEV).requires_grad_(True)
     assert loss_head.eligible(ode, lat, lin, S, B)
     nll, reg = loss_head.fused_loss_head(ode, lat, lin, y.to(DEV), S, B)
-    g_nll, g_reg = 0.7, 0.1
-    (g_nll * nll + g_reg * reg).backward()
-    rn, rr, rl, rW, rb = _reference(latent, W, b, y, S, B, g_nll, g_reg)
-    assert normwise_rel(nll, rn) < 1e-5 and normwise_rel(reg, rr) < 1e-5
-    assert normwise_rel(lat.grad, rl) < 1e-5
-    assert torch.equal(lat.grad[..., 3:].cpu(), torch.zeros_like(rl[..., 3:]).float())
-    assert normwise_rel(lin.weight.grad, rW) < 1e-5 and normwise_rel(lin.bias.grad, rb) < 1e-5
+    (g["meta"]["g_nll"] * nll + g["meta"]["g_reg"] * reg).backward()
+    assert normwise_rel(nll, g["nll"]) < 1e-5 and normwise_rel(reg, g["reg"]) < 1e-5
+    assert normwise_rel(lat.grad[..., :3], g["dlat3"]) < 1e-5
+    assert int(torch.count_nonzero(lat.grad[..., 3:])) == 0
+    assert normwise_rel(lin.weight.grad, g["dW"]) < 1e-5 and normwise_rel(lin.bias.grad, g["db"]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_loss_head_rejects_oversized_sample_tile(pkg):
+    """S = 129 exceeds the kernel's sample tile: not eligible, so VAE.calc_loss takes the
+    reference's own ops (it used to raise from the C-ABI)."""
+    from ude_amd import loss_head
+    R, L, T, S, B = 1, 8, 3, 129, 2
+    ode = _ode_for(pkg, R, L)
+    lin = torch.nn.Linear(3, 1).to(DEV)
+    lat = torch.rand(T, S * B, R, L, device=DEV)
+    assert not loss_head.eligible(ode, lat, lin, S, B)
+    assert not loss_head.eligible(ode, lat[..., 1:], lin, S, B)              # not the model's L
+
+
+def _vae_step(S, fused_ok, monkeypatch):
+    import lib.VAE as vae_mod
+    import lib.models as models
+    from ude_amd import loss_head
+    torch.manual_seed(3)
+    model = vae_mod.VAE(models.Encoder_Back_GRU, models.FaFp, models.Decoder, 4, 8, 1,
+                        ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
+                        enc_params={"q_sizes": [16, 8], "ff_sizes": [8], "SIR_scaler": [0.1, 0.05, 1.0]})
+    model.to(DEV)
+    model.setup_training()
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(3, 6, 5, generator=gen).to(DEV)
+    y = (torch.rand(3, 3, 1, generator=gen) * 0.5).to(DEV)
+    t = torch.arange(3, dtype=torch.float32)
+    eps = torch.randn(S, 3, 1, 7, generator=gen).to(DEV)
+    if not fused_ok:
+        monkeypatch.setattr(loss_head, "eligible", lambda *a, **k: False)
+    real_randn = torch.randn
+    monkeypatch.setattr(torch, "randn", lambda *a, **k: eps.clone())
+    y_pred = model(x, t, n_samples=S, training=True)
+    monkeypatch.setattr(torch, "randn", real_randn)
+    losses = {"nll": True, "mse": False, "kl_z": True, "kl_p": True, "Fa_norm": 0.1, "reg_loss": True,
+              "anneal": True}
+    took_fused = model._fused_head(y_pred, y, losses) is not None
+    loss, data, names = model.calc_loss(y_pred, y, losses)
+    loss.backward()
+    monkeypatch.undo()
+    grads = {f"{part}.{k}": p.grad.detach().clone() for part in ("enc", "ode", "dec")
+             for k, p in getattr(model, part).named_parameters()}
+    return took_fused, loss.detach(), grads
+
+
+@pytest.mark.gpu
+def test_vae_calc_loss_fused_head_matches_eager(pkg, monkeypatch):
+    """One batch through VAE.calc_loss with the fused head and with the reference's ops
+    (loss_head disabled): the loss and every gradient agree to 1e-5."""
+    f_on, loss_f, g_f = _vae_step(64, True, monkeypatch)
+    f_off, loss_e, g_e = _vae_step(64, False, monkeypatch)
+    assert f_on and not f_off
+    assert normwise_rel(loss_f, loss_e) < 1e-5
+    for k in g_e:
+        assert normwise_rel(g_f[k], g_e[k]) < 1e-5, (k, normwise_rel(g_f[k], g_e[k]))
+
+
+@pytest.mark.gpu
+def test_vae_calc_loss_large_sample_count_runs_eager(pkg, monkeypatch):
+    """n_samples = 129 (> the kernel's 128 tile): calc_loss takes the reference's ops, no error."""
+    took_fused, loss, grads = _vae_step(129, True, monkeypatch)
+    assert not took_fused and torch.isfinite(loss)

@@ -172,6 +172,73 @@ __device__ __forceinline__ float elu1(float x) {
 template <class M, int NZ_>
 using C1Arr = f4[NZ_ > 0 ? NZ_ : 1];
 
+// Input-gradient (dX) fragments of wave W at depth d: [XQ(W, d)] quads in tile order.
+template <class M, int W, int d>
+__device__ __forceinline__ void load_x_frags(Rsrc rs, int lane, f4* fx) {
+  if constexpr (d == 0 && M::SPLITX0) {
+    // wave W's K quads qq = W (mod WAVES) of every layer-0 input tile m (merged nets, P first)
+    constexpr int PQ = M::HAS_P ? M::kout(0, 0) / 16 : 0;
+    sfor<M::XT(0)>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      sfor<M::x0q_w(W)>([&](auto jj) {
+        constexpr int j = decltype(jj)::value, qq = W + j * WAVES;
+        constexpr int net = qq < PQ ? 0 : 1, q = qq < PQ ? qq : qq - PQ;
+        fx[m * M::x0q_w(W) + j] =
+            ldw(rs, lane * 16, (M::wt_off(net, 0) + m * (M::kout(net, 0) / 16) * 256 + q * 256) * 4);
+      });
+    });
+    return;
+  }
+  sfor<M::XT(d)>([&](auto mm) {
+    constexpr int m = decltype(mm)::value;
+    if constexpr (M::xowner(d, m) == W) {
+      constexpr int q0 = M::xq_before(W, d, m);
+      if constexpr (d == 0) {
+        if constexpr (M::HAS_P)
+          load_frags<M::kout(0, 0), M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256>(rs, lane, fx + q0);
+        if constexpr (M::HAS_A)
+          load_frags<M::kout(1, 0), M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256>(
+              rs, lane, fx + q0 + (M::HAS_P ? M::kout(0, 0) / 16 : 0));
+      } else {
+        constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
+        load_frags<M::kout(net, d), M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256>(rs, lane, fx + q0);
+      }
+    }
+  });
+}
+
+// Register-resident weights (Model::WREG): every fragment / bias quad wave W reads in the
+// forward (and, BWD, the input-gradient fragments), loaded once per launch.
+struct NoWRegs {
+  static constexpr bool ON = false;
+  f4 wf[1], wb[1], wx[1];
+};
+template <class M, int W, bool BWD>
+struct WRegs {
+  static constexpr bool ON = M::WREG;
+  static constexpr int NF = ON ? M::WF_Q(W) : 0, NB = ON ? M::WB_Q(W) : 0, NX = (ON && BWD) ? M::WX_Q(W) : 0;
+  f4 wf[NF > 0 ? NF : 1], wb[NB > 0 ? NB : 1], wx[NX > 0 ? NX : 1];
+  __device__ __forceinline__ void load(Rsrc rs, int lane) {
+    if constexpr (ON) {
+      const int g = lane >> 4;
+      sfor<M::D>([&](auto dd) {
+        constexpr int d = decltype(dd)::value;
+        sfor<M::FT(d)>([&](auto kk) {
+          constexpr int k = decltype(kk)::value;
+          if constexpr (M::fowner(d, k) == W) {
+            constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
+            load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane,
+                                                                     wf + M::fq_base(W, d) + M::fq_before(W, d, k));
+            if constexpr (M::has_bias(d))
+              wb[M::nb_base(W, d) + M::nb_before(W, d, k)] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
+          }
+        });
+        if constexpr (BWD) load_x_frags<M, W, d>(rs, lane, wx + M::xq_base(W, d));
+      });
+    }
+  }
+};
+
 // Forward pass of both MLPs for the stage input held in the record's Y slot.
 // Leaves post-activation outputs of every layer in the record (the final
 // layers' raw outputs: P-net pre-|.| rates q, A-net Fa).  Ends on a barrier.
@@ -182,9 +249,10 @@ struct NoHook {
 
 // `hook(integral_constant<d>)` runs right after phase d's weight loads are issued
 // (used by the backward to start HBM loads early without holding registers long).
-template <class M, int W, int SR, class Hook = NoHook>
-__device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, int lane, Prof* pf = nullptr,
-                                            const Hook& hook = Hook{}) {
+template <class M, int W, int SR, class WR = NoWRegs, class Hook = NoHook>
+__device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, int lane, const WR& wr = WR{},
+                                            Prof* pf = nullptr, const Hook& hook = Hook{}) {
+  constexpr bool RW = WR::ON;
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto dd) {
@@ -192,15 +260,21 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     constexpr int NF = M::FQ(W, d);
     // all of this wave's weight fragments (and biases) for the phase are in flight
     // before its first MFMA
-    f4 fr[NF > 0 ? NF : 1], bias[M::FT(d) > 0 ? M::FT(d) : 1];
-    sfor<M::FT(d)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(d, k) == W) {
-        constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
-        load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
-        if constexpr (!(d == 0 && M::HOIST)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
-      }
-    });
+    f4 fr[(NF > 0 && !RW) ? NF : 1], bias[(M::FT(d) > 0 && !RW) ? M::FT(d) : 1];
+    if constexpr (!RW) {
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
+          load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
+          if constexpr (M::has_bias(d)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
+        }
+      });
+    }
+    auto FR = [&](int i) -> f4 {
+      if constexpr (RW) return wr.wf[M::fq_base(W, d) + i];
+      else return fr[i];
+    };
     hook(dd);
     __builtin_amdgcn_sched_barrier(0);
     f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
@@ -208,6 +282,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
         if constexpr (d == 0 && M::HOIST) acc[k] = c1[M::nz_before(W, k)];
+        else if constexpr (RW) acc[k] = wr.wb[M::nb_base(W, d) + M::nb_before(W, d, k)];
         else acc[k] = bias[k];
       }
     });
@@ -235,7 +310,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
               sfor<M::FT(d)>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
                 if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net)
-                  acc[k] = mfma4(fr[M::fq_before(W, d, k) + q][e], x[e], acc[k]);
+                  acc[k] = mfma4(FR(M::fq_before(W, d, k) + q)[e], x[e], acc[k]);
               });
           }
         }
@@ -317,6 +392,9 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
   double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
 
+  WRegs<M, W, false> wr;
+  wr.load(rs, lane);
+
   #pragma unroll 1
   for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
   __syncthreads();
@@ -358,7 +436,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         // BAYES: evaluation 4 step + j has its own weight sample
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
-        mlp_forward<M, W, SR>(rse, lds, c1, lane);
+        mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
         sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
@@ -517,32 +595,22 @@ struct RkAdjointEp {
 // BAYES: `es` addresses this evaluation's eps in slab order; every tile's dW
 // contribution of the evaluation is also accumulated eps-weighted into `dws` (and the
 // bias row sums into DBS): d|std| = sum_eval eps_eval * dW_eval (models_bayes.py:45-46).
-template <class M, int W, int SR, class DW, class DS, class G0, class EP0>
+template <class M, int W, int SR, class DW, class DS, class G0, class EP0, class WR>
 __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
-                                             Prof* pf, const EP0& ep0) {
+                                             Prof* pf, const EP0& ep0, const WR& wr) {
+  constexpr bool RW = WR::ON;
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
     constexpr int d = M::D - 1 - decltype(ee)::value;
     // input-gradient fragments go out first; the LDS-only dW GEMMs below hide them
     constexpr int NX = M::XQ(W, d);
-    f4 fx[NX > 0 ? NX : 1];
-    sfor<M::XT(d)>([&](auto mm) {
-      constexpr int m = decltype(mm)::value;
-      if constexpr (M::xowner(d, m) == W) {
-        constexpr int q0 = M::xq_before(W, d, m);
-        if constexpr (d == 0) {
-          if constexpr (M::HAS_P)
-            load_frags<M::kout(0, 0), M::wt_off(0, 0) + m * (M::kout(0, 0) / 16) * 256>(rs, lane, fx + q0);
-          if constexpr (M::HAS_A)
-            load_frags<M::kout(1, 0), M::wt_off(1, 0) + m * (M::kout(1, 0) / 16) * 256>(
-                rs, lane, fx + q0 + (M::HAS_P ? M::kout(0, 0) / 16 : 0));
-        } else {
-          constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
-          load_frags<M::kout(net, d), M::wt_off(net, d) + rt * (M::kout(net, d) / 16) * 256>(rs, lane, fx + q0);
-        }
-      }
-    });
+    f4 fx[(NX > 0 && !RW) ? NX : 1];
+    if constexpr (!RW) load_x_frags<M, W, d>(rs, lane, fx);
+    auto FX = [&](int i) -> f4 {
+      if constexpr (RW) return wr.wx[M::xq_base(W, d) + i];
+      else return fx[i];
+    };
     // BAYES: this evaluation's eps for the wave's dW tiles (C layout) and bias rows
     constexpr int NE = M::BAYES ? M::ndw_phase(W, d) : 0;
     f4 ef[NE > 0 ? NE : 1], eb[M::FT(d) > 0 ? M::FT(d) : 1];
@@ -634,6 +702,31 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
     // (2) gradient w.r.t. the layer input (rows = input features); tiles sharing a
     // B operand (the same net's output gradient) are interleaved
     f4 xa[M::XT(d) > 0 ? M::XT(d) : 1];
+    if constexpr (d == 0 && M::SPLITX0) {
+      // partial input gradient of every layer-0 tile over this wave's K quads, to LDS;
+      // summed (fixed wave order) and fed to the RK adjoint by bwd_body after the barrier
+      constexpr int PQ = M::HAS_P ? M::kout(0, 0) / 16 : 0;
+      sfor<M::XT(0)>([&](auto mm) { xa[decltype(mm)::value] = f4zero(); });
+      sfor<M::x0q_w(W)>([&](auto jj) {
+        constexpr int j = decltype(jj)::value, qq = W + j * WAVES;
+        constexpr int net = qq < PQ ? 0 : 1, q = qq < PQ ? qq : qq - PQ;
+        constexpr int KP = M::kout(net, 0);
+        const f4 x = *reinterpret_cast<const f4*>(rec + M::gbuf(net, 0) + g * (KP / 4) + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          sfor<M::XT(0)>([&](auto mm) {
+            constexpr int m = decltype(mm)::value;
+            xa[m] = mfma4(FX(m * M::x0q_w(W) + j)[e], x[e], xa[m]);
+          });
+      });
+      sfor<M::XT(0)>([&](auto mm) {
+        constexpr int m = decltype(mm)::value;
+        *reinterpret_cast<f4*>(lds + M::X0P_LDS + ((W * M::XT(0) + m) * 64 + lane) * 4) = xa[m];
+      });
+      __syncthreads();
+      UDE_STAMP(pf, 7 + d);
+      return;
+    }
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) xa[m] = f4zero();
@@ -657,7 +750,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
             sfor<M::XT(d)>([&](auto mm) {
               constexpr int m = decltype(mm)::value;
               if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net))
-                xa[m] = mfma4(fx[M::xq_before(W, d, m) + qoff + q][e], x[e], xa[m]);
+                xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
             });
         }
       }
@@ -919,6 +1012,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   }
 #endif
 
+  WRegs<M, W, true> wr;
+  wr.load(rs, lane);
+
   #pragma unroll 1
   for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;
   __syncthreads();
@@ -1033,7 +1129,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           rse = make_rsrc(A.pack + ev * M::PACK_TOTAL, M::PACK_TOTAL * 4);
           es = make_rsrc(A.eslab + ev * M::SLAB_TOTAL, M::SLAB_TOTAL * 4);
         }
-        mlp_forward<M, W, SR>(rse, lds, c1, lane, pf, [&](auto dd) {
+        // the next stage's checkpointed input: small records (one pair slot per thread)
+        // fetch it before the recomputed forward, whose phases then hide the HBM latency;
+        // wide ones under the flux pass (registers only live across that pass)
+        float ckn[SL][3], sgn[SL][3], pgn[SL][3];
+        constexpr bool EARLY_CK = SL == 1;
+        if (EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
           if constexpr (decltype(dd)::value == (M::D > 2 ? 1 : 0))
             if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
         });
@@ -1041,10 +1143,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
-        // the next stage's checkpointed input is fetched under the flux pass and the
-        // MLP backward (registers only live across the flux pass)
-        float ckn[SL][3], sgn[SL][3], pgn[SL][3];
-        if (have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
         flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         if (next_out) {
           out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
@@ -1094,7 +1193,33 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);
-        mlp_backward<M, W, SR>(rse, es, lds, dw, dws, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj});
+        mlp_backward<M, W, SR>(rse, es, lds, dw, dws, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
+        if constexpr (M::SPLITX0) {
+          // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
+          // use the step-end thread <-> (t, quad) mapping, so the step end needs no barrier.
+          auto x0sum = [&](int t, int f0) {
+            const int m = f0 >> 4, li = ((f0 >> 2) & 3) * 16 + t;
+            f4 v = f4zero();
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w)
+              v += *reinterpret_cast<const f4*>(lds + M::X0P_LDS + ((w * M::XT(0) + m) * 64 + li) * 4);
+            return v;
+          };
+          constexpr int NV = M::F4 / 4, NVX = cmin(M::F4, M::F16) / 4;
+          #pragma unroll 1
+          for (int i = tid; i < TT * NV; i += NTHREADS) {
+            const int t = i / NV, v = i - t * NV;
+            if (v < NVX) RkAdjointEp<M, SR>{lds + t * SR, dt, jj}(4 * v, x0sum(t, 4 * v));
+          }
+          if constexpr (M::FULL0) {
+            constexpr int NS = M::S16 / 4;
+            #pragma unroll 1
+            for (int i = tid; i < TT * NS; i += NTHREADS) {
+              const int t = i / NS, v = i - t * NS;
+              RkAdjointEp<M, SR>{lds + t * SR, dt, jj}(M::F16 + 4 * v, x0sum(t, M::F16 + 4 * v));
+            }
+          }
+        }
 
         UDE_STAMP(pf, 12);
       }

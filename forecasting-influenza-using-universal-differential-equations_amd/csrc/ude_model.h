@@ -143,7 +143,9 @@ struct Model {
   // + staging slot for the next stage's checkpointed input ([t][F4], prefetched
   // during the flux pass)
   static constexpr int STG_LDS = DB_LDS + (BAYES ? 2 : 1) * NDB;
-  static constexpr int LDS_B = (STG_LDS + TT * F4) * 4;
+  // SPLITX0: per-wave partial layer-0 input-gradient tiles [WAVES][XT(0)][64 lanes][4]
+  static constexpr int X0P_LDS = STG_LDS + TT * F4;
+  static constexpr int LDS_B = (X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");
 
   // ---- packed weights (fragment order, 16-B per lane per MFMA quad) --------------
@@ -254,12 +256,48 @@ struct Model {
   static constexpr int xq(int d, int m) {
     return d == 0 ? (HAS_P ? kout(0, 0) / 16 : 0) + (HAS_A ? kout(1, 0) / 16 : 0) : kout(xnet(d, m), d) / 16;
   }
+  // Layer-0 input gradient with fewer feature tiles than waves (small R): instead of one
+  // wave running a tile's whole K = K0 chain, every wave takes the K quads qq = w (mod 4) of
+  // every tile and the 4 partial tiles are summed afterwards (bwd_body, fixed order).
+  static constexpr int X0Q = (HAS_P ? kout(0, 0) / 16 : 0) + (HAS_A ? kout(1, 0) / 16 : 0);
+  static constexpr bool SPLITX0 = XT(0) < WAVES;
+  static constexpr int x0q_w(int w) { int s = 0; for (int qq = 0; qq < X0Q; ++qq) if (qq % WAVES == w) s += 1; return s; }
   static constexpr int xq_before(int w, int d, int m) {
+    if (d == 0 && SPLITX0) return m * x0q_w(w);
     int s = 0;
     for (int mm = 0; mm < m; ++mm) if (xowner(d, mm) == w) s += xq(d, mm);
     return s;
   }
   static constexpr int XQ(int w, int d) { return xq_before(w, d, XT(d)); }
+
+  // ---- register-resident weights (small models) ---------------------------------
+  // A wave's weight fragments never change during a launch (deterministic RHS): when all
+  // of them fit next to the working set they are loaded once into VGPRs instead of being
+  // re-read from L2 at every layer phase (at R = 1 that L2 latency, not the MFMA work,
+  // paced every phase).  Per wave: forward fragments, bias quads, input-gradient fragments.
+  static constexpr bool has_bias(int d) { return !(d == 0 && HOIST); }
+  static constexpr int nb_phase(int w, int d) {
+    int s = 0;
+    if (has_bias(d))
+      for (int k = 0; k < FT(d); ++k) if (fowner(d, k) == w) s += 1;
+    return s;
+  }
+  static constexpr int nb_before(int w, int d, int k) {
+    int s = 0;
+    if (has_bias(d))
+      for (int kk = 0; kk < k; ++kk) if (fowner(d, kk) == w) s += 1;
+    return s;
+  }
+  static constexpr int fq_base(int w, int d) { int s = 0; for (int e = 0; e < d; ++e) s += FQ(w, e); return s; }
+  static constexpr int nb_base(int w, int d) { int s = 0; for (int e = 0; e < d; ++e) s += nb_phase(w, e); return s; }
+  static constexpr int xq_base(int w, int d) { int s = 0; for (int e = 0; e < d; ++e) s += XQ(w, e); return s; }
+  static constexpr int WF_Q(int w) { return fq_base(w, D); }
+  static constexpr int WB_Q(int w) { return nb_base(w, D); }
+  static constexpr int WX_Q(int w) { return xq_base(w, D); }
+  static constexpr int wreg_q(int w) { return WF_Q(w) + WB_Q(w) + WX_Q(w); }
+  static constexpr int max_wreg_q() { return cmax(cmax(wreg_q(0), wreg_q(1)), cmax(wreg_q(2), wreg_q(3))); }
+  static constexpr int WREG_MAX_Q = 56;      // <= 224 VGPRs of resident fragments per wave
+  static constexpr bool WREG = !BAYES && max_wreg_q() <= WREG_MAX_Q;
 
   // ---- parameters in torch order (nn.Linear weight (out,in) then bias) ----------------
   static constexpr int param_w_off(int net, int i) {

@@ -63,8 +63,11 @@ def _stream(device) -> int:
 
 
 class FusedRK4(torch.autograd.Function):
+    """Returns (latent, stats, ckpt); ckpt (the stage inputs of every step) is only a real
+    output when keep_ckpt is set (materialised tracking), else an empty tensor."""
+
     @staticmethod
-    def forward(ctx, plan: Plan, y0: torch.Tensor, *params: torch.Tensor):
+    def forward(ctx, plan: Plan, y0: torch.Tensor, keep_ckpt: bool, *params: torch.Tensor):
         dev = y0.device
         stream = _stream(dev)
         sz = plan.sizes
@@ -74,7 +77,8 @@ class FusedRK4(torch.autograd.Function):
         plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
         latent = torch.empty((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         need_grad = any(ctx.needs_input_grad[1:])
-        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) if need_grad else None
+        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
+            if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
         stats = torch.zeros(5, dtype=torch.float32, device=dev)
         if EVENTS is not None:
@@ -86,10 +90,12 @@ class FusedRK4(torch.autograd.Function):
         ctx.plan = plan
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
-        return latent, stats
+        out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
+        ctx.mark_non_differentiable(out_ck)
+        return latent, stats, out_ck
 
     @staticmethod
-    def backward(ctx, dlatent, dstats):
+    def backward(ctx, dlatent, dstats, _dckpt=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats = ctx.saved_tensors
         dev = y0.device
@@ -108,7 +114,7 @@ class FusedRK4(torch.autograd.Function):
                           dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
-        return (None, dy0) + tuple(_split(dparams, plan.param_shapes))
+        return (None, dy0, None) + tuple(_split(dparams, plan.param_shapes))
 
 
 def _split(flat: torch.Tensor, shapes) -> List[torch.Tensor]:

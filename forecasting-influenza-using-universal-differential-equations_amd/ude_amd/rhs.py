@@ -58,11 +58,42 @@ def _finish(flux3: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return res
 
 
+class _FusedList(list):
+    """Per-evaluation entries materialised from a fused solve (``materialize_tracking``): the
+    reference's list contents for readers; ``posterior()`` takes the same evaluations from the
+    solve's exact sufficient statistics instead, so they are not counted twice."""
+
+
+class _TrackerView(torch.autograd.Function):
+    """Materialised A-net outputs of every evaluation (E, N, R, 3) whose gradient is handed to
+    the solve as d |Fa| (the kernel back-propagates d|Fa|/dFa = Fa / |Fa| through every
+    evaluation).  Exact for functions of the norm, torch.norm(torch.stack(tracker)) being the
+    reference's only use (lib/VAE.py:180); other functions of the entries get that projection."""
+
+    @staticmethod
+    def forward(ctx, stats, fa_all):
+        ctx.save_for_backward(stats, fa_all)
+        return fa_all.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        stats, fa_all = ctx.saved_tensors
+        nrm = stats[4]
+        d = torch.zeros_like(stats)
+        d[4] = torch.where(nrm > 0, (g.double() * fa_all.double()).sum() / nrm.double(),
+                           torch.zeros((), dtype=torch.float64, device=g.device)).to(stats.dtype)
+        return d, None
+
+
 class _UDEModule(nn.Module):
     """Shared tracking / posterior logic of the three RHS classes."""
 
     ode_type = "FaFp"
     uncertainty = "none"
+    # opt-in: after a fused solve, fill ``params`` / ``tracker`` with one (N, R, 2) rate tensor /
+    # one (N, R, 3) A-net tensor per RHS evaluation, as the reference's forward appends them
+    # (lib/models.py:137, :187, :238, :252); recomputed from the solve's stage checkpoints
+    materialize_tracking = False
 
     def _init_tracking(self):
         self.params = []
@@ -76,19 +107,50 @@ class _UDEModule(nn.Module):
         self._fused_rates = []
 
     # -- fused-solver side statistics ------------------------------------------
-    def _record_fused(self, stats: torch.Tensor, n_eval: int) -> None:
-        """stats = [mean_b, mean_g, std_b, std_g, |Fa|] from one fused solve."""
+    def _record_fused(self, stats: torch.Tensor, n_eval: int, evals=None) -> None:
+        """stats = [mean_b, mean_g, std_b, std_g, |Fa|] from one fused solve; evals = the
+        materialised (rates (E, N, R, 2), Fa (E, N, R, 3)) of its evaluations, or None."""
         if self.ode_type in ("Fp", "FaFp"):
             self._fused_rates.append((float(n_eval), stats[0:2], stats[2:4]))
+            if evals is not None:
+                if not isinstance(self.params, _FusedList):
+                    self.params = _FusedList(self.params)
+                self.params.extend(evals[0].unbind(0))
         if self.ode_type in ("Fa", "FaFp"):
-            # torch.norm(torch.stack(tracker)) over this entry == |Fa| of the solve,
-            # and over several entries == the norm of all of them together.
-            self.tracker.append(stats[4:5])
+            if evals is not None:
+                self.tracker.extend(_TrackerView.apply(stats, evals[1]).unbind(0))
+            else:
+                # torch.norm(torch.stack(tracker)) over this entry == |Fa| of the solve,
+                # and over several entries == the norm of all of them together.
+                self.tracker.append(stats[4:5])
+
+    @torch.no_grad()
+    def _evals_from_checkpoint(self, ckpt: torch.Tensor, y0: torch.Tensor, n_steps: int, chunk: int = 64):
+        """Every evaluation's rates / A-net output, recomputed from the stage inputs the
+        training forward checkpoints ([tile][step][stage][3R][16], include/ude_rk4.h) and the
+        static latent dims of y0."""
+        N, R, L = y0.shape
+        tiles = (N + 15) // 16
+        E = 4 * n_steps
+        dyn = ckpt[: tiles * n_steps * 4 * 3 * R * 16].view(tiles, E, 3 * R, 16)
+        static = y0.detach()[..., 3:]
+        rates = torch.empty((E, N, R, 2), dtype=y0.dtype, device=y0.device) if self.ode_type != "Fa" else None
+        fas = torch.empty((E, N, R, 3), dtype=y0.dtype, device=y0.device) if self.ode_type != "Fp" else None
+        for e0 in range(0, E, chunk):
+            e1 = min(E, e0 + chunk)
+            d = dyn[:, e0:e1].permute(1, 0, 3, 2).reshape(e1 - e0, tiles * 16, R, 3)[:, :N]
+            x = torch.cat([d, static.unsqueeze(0).expand(e1 - e0, N, R, L - 3)], -1).reshape(-1, R, L)
+            if rates is not None:
+                rates[e0:e1] = torch.abs(_run_stack(self._p_stack(), x)).reshape(e1 - e0, N, R, 2)
+            if fas is not None:
+                h = x if self.ode_type == "FaFp" else self.flatten(x)
+                fas[e0:e1] = _run_stack(self._a_stack(), h).reshape(e1 - e0, N, R, 3)
+        return rates, fas
 
     def posterior(self) -> Normal:
         """Normal(mean, unbiased std) of every recorded rate; clears them (:152-156)."""
         groups = []
-        if self.params:
+        if self.params and not isinstance(self.params, _FusedList):
             p = torch.stack(self.params).reshape(-1, 2)
             groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
         groups.extend(self._fused_rates)

@@ -125,10 +125,16 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
     if bayes:
         n_par = sum(int(p.numel()) for p in mus)
         eps = func.take_eps(4 * plan.prob.n_steps, n_par, y0.device)
+        if func.materialize_tracking:
+            raise NotImplementedError("materialize_tracking: Bayesian RHS (per-evaluation weight samples) "
+                                      "is not supported")
         latent, stats = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *params)
+        func._record_fused(stats, plan.n_eval)
     else:
-        latent, stats = _fused.FusedRK4.apply(plan, y0.contiguous(), *params)
-    func._record_fused(stats, plan.n_eval)
+        keep = bool(func.materialize_tracking)
+        latent, stats, ckpt = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
+        evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps) if keep else None
+        func._record_fused(stats, plan.n_eval, evals)
     return latent
 
 

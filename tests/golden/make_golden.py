@@ -328,12 +328,22 @@ def make_e2e_us():
                   seed=1111)
 
 
+def make_e2e_toy64():
+    # the toy shapes of e2e_vae_step (S = 5, masked target), with the fp64 parity target
+    make_e2e_case("e2e_vae_toy64", R=1, n_qs=3, B=4, S_=5, window=6, gamma=21,
+                  ode_params={"net_sizes": [16, 16, 8], "aug_net_sizes": [16, 12]},
+                  enc_params={"q_sizes": [16, 8], "ff_sizes": [8, 8], "SIR_scaler": [0.1, 0.05, 1.0]},
+                  seed=4242)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(1)
     if len(sys.argv) > 1 and sys.argv[1] == "e2e_state49":
         make_e2e_state49()
     elif len(sys.argv) > 1 and sys.argv[1] == "e2e_us":
         make_e2e_us()
+    elif len(sys.argv) > 1 and sys.argv[1] == "e2e_toy64":
+        make_e2e_toy64()
     else:
         if len(sys.argv) == 1:
             main()

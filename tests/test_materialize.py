@@ -1,0 +1,83 @@
+"""Opt-in materialised tracking lists: with ``ode.materialize_tracking =
+True`` a fused solve fills ``ode.params`` / ``ode.tracker`` with one entry per RHS
+evaluation, as the reference's forward appends them (lib/models.py:137, :187, :238, :252),
+while posterior() and the tracker norm keep back-propagating into the kernel.
+
+Checked against the eager (per-evaluation) solve of the same module: every entry, the
+posterior, the norm, and all gradients."""
+import pytest
+import torch
+
+from helpers import normwise_rel
+
+
+def _case(pkg, kind, dev):
+    torch.manual_seed(11)
+    if kind == "FaFp":
+        mod = pkg.FaFp(3, latent_dim=5, net_sizes=[40, 24], aug_net_sizes=[36])
+        mod.Fa_w = 0.5
+    elif kind == "Fp":
+        mod = pkg.Fp(1, latent_dim=8, net_sizes=[64, 64, 32])
+    else:
+        mod = pkg.Fa(1, latent_dim=8, aug_net_sizes=[64, 64])
+    gen = torch.Generator().manual_seed(12)
+    R, L = mod.n_regions, mod.latent_dim
+    N = 37
+    S = torch.rand(N, R, generator=gen) * 0.4 + 0.5
+    I = torch.rand(N, R, generator=gen) * 0.05
+    y0 = torch.cat([S[..., None], I[..., None], (1 - S - I)[..., None], torch.randn(N, R, L - 3, generator=gen)], -1)
+    t = torch.arange(7, dtype=torch.float32) / 3.0
+    return mod.to(dev), y0.to(dev).requires_grad_(True), t
+
+
+def _solve(pkg, mod, y0, t, materialize):
+    mod.materialize_tracking = materialize
+    mod.clear_tracking()
+    mod.zero_grad(set_to_none=True)
+    y0.grad = None
+    lat = pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+    params = [p.detach().clone() for p in mod.params]
+    loss = 0.01 * lat.sum()
+    post = None
+    if mod.ode_type != "Fa":
+        post = mod.posterior()
+        loss = loss + (post.loc * torch.tensor([0.3, -0.2], device=y0.device)).sum() \
+            + (post.scale * torch.tensor([0.5, 0.1], device=y0.device)).sum()
+    tracker = [x.detach().clone() for x in mod.tracker]
+    nrm = None
+    if mod.ode_type != "Fp":
+        nrm = torch.norm(torch.stack(mod.tracker))
+        loss = loss + 0.1 * nrm
+    loss.backward()
+    grads = {"y0": y0.grad.clone(), **{k: p.grad.clone() for k, p in mod.named_parameters()}}
+    return params, tracker, post, nrm, grads
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["FaFp", "Fp", "Fa"])
+def test_materialized_lists_match_eager_solve(pkg, kind):
+    mod, y0, t = _case(pkg, kind, "cuda")
+    p_f, tr_f, post_f, nrm_f, g_f = _solve(pkg, mod, y0, t, True)
+    n_eval = 4 * (len(t) - 1)
+    # the eager solve of the same module on the host appends one entry per evaluation
+    mod_c, y0_c, _ = _case(pkg, kind, "cpu")
+    mod_c.load_state_dict({k: v.cpu() for k, v in mod.state_dict().items()})
+    if kind == "FaFp":
+        mod_c.Fa_w = mod.Fa_w
+    p_e, tr_e, post_e, nrm_e, g_e = _solve(pkg, mod_c, y0_c, t, False)
+    if kind != "Fa":
+        assert len(p_f) == len(p_e) == n_eval
+        for a, b in zip(p_f, p_e):
+            assert a.shape == b.shape and normwise_rel(a, b) < 1e-5
+        assert normwise_rel(post_f.loc, post_e.loc) < 1e-5 and normwise_rel(post_f.scale, post_e.scale) < 1e-5
+    if kind != "Fp":
+        assert len(tr_f) == len(tr_e) == n_eval
+        for a, b in zip(tr_f, tr_e):
+            assert a.shape == b.shape and normwise_rel(a, b) < 1e-5
+        assert normwise_rel(nrm_f, nrm_e) < 1e-5
+    for k in g_e:
+        assert normwise_rel(g_f[k], g_e[k]) < 5e-5, (k, normwise_rel(g_f[k], g_e[k]))
+    # and the same gradients as the default (statistics-only) fused solve
+    _, _, _, _, g_s = _solve(pkg, mod, y0, t, False)
+    for k in g_s:
+        assert normwise_rel(g_f[k], g_s[k]) < 1e-5, k

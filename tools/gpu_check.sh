@@ -1,10 +1,17 @@
+# GPU-box check used during development: parity tests, bench line, M1 stage profile + rocprof.
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
-tail -30 gpurun_out/pytest_gpu.log
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
-rc=$?
-tail -c 3000 gpurun_out/bench.json
+grep -E "passed|failed" gpurun_out/pytest_gpu.log | tail -3
+grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -20
+[ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+tail -c 1500 gpurun_out/bench.json
+if [ "$1" = "prof" ]; then
+  timeout -k 10 120 python -u tools/stage_profile.py us_northstar > gpurun_out/stage_m1.txt 2>&1 || exit $?
+  cat gpurun_out/stage_m1.txt
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_m1 -o m1 -- python3 bench.py --workload us_northstar --steps 5 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/prof_m1.log 2>&1 || exit $?
+fi
 exit $rc

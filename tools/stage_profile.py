@@ -24,11 +24,15 @@ SEG = {0: "stage input (ckpt)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1
 
 
 def main():
-    wl = sys.argv[1] if len(sys.argv) > 1 else "state49"
+    wl = sys.argv[1] if len(sys.argv) > 1 else "state49"      # [--build]: compile only (on the host)
     w = bench.WORKLOADS[wl]
     cfg = (w["kind"], w["R"], w["L"], tuple(w["net"]) if w["net"] else None, tuple(w["aug"]) if w["aug"] else None)
-    path = os.path.join(_native.BUILD, "libude_rk4_profile.so")
-    _native.build_library([cfg], path, "profile", jobs=1, extra_flags=["-DUDE_PROFILE"])
+    path = os.path.join(_native.BUILD, f"libude_rk4_profile_{wl}.so")
+    if "--build" in sys.argv or not os.path.exists(path):
+        _native.build_library([cfg], path, "profile_" + wl, jobs=1, extra_flags=["-DUDE_PROFILE"])
+        if "--build" in sys.argv:
+            print("built", path)
+            return
     lib = _native.NativeLib(path)
     lib.lib.ude_debug_set_prof.argtypes = [ctypes.c_void_p]
     _native.library_for = lambda c: lib

@@ -179,9 +179,9 @@ struct Ops {
   }
 
   static int backward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
-                      const float* ckpt, const float* dlatent, const float* stats_out, const float* dstats,
-                      float* dy0, float* slab, float* dparams, hipStream_t s) {
-    if (!pack || !sched || !y0 || !dlatent || !stats_out || !dstats || !dy0 || !slab || !dparams) return UDE_E_INVALID;
+                      const float* ckpt, const float* dlatent, const float* dlat_sir, const float* stats_out,
+                      const float* dstats, float* dy0, float* slab, float* dparams, hipStream_t s) {
+    if (!pack || !sched || !y0 || !stats_out || !dstats || !dy0 || !slab || !dparams) return UDE_E_INVALID;
     if (p->n_steps > 0 && !ckpt) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -192,7 +192,7 @@ struct Ops {
     KArgs a;
     memset(&a, 0, sizeof(a));
     a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
-    a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.stats_out = stats_out; a.dstats = dstats;
+    a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.dlat_sir = dlat_sir; a.stats_out = stats_out; a.dstats = dstats;
     a.dy0 = dy0; a.slab = slab;
     if (M::BAYES) a.eslab = pack + (size_t)n_evals(p) * M::PACK_TOTAL;
     float* g0buf = slab + (size_t)gb * M::SLAB_STRIDE;
@@ -383,7 +383,8 @@ struct LossOps {
     return UDE_OK;
   }
   static int run(bool bwd, int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
-                 const float* grad, void* ws, float* out, float* dlatent, float* dW, float* db, hipStream_t s) {
+                 const float* grad, void* ws, float* out, float* dlatent, float* dW, float* db, hipStream_t s,
+                 int dl_sir = 0) {
     if (!latent || !W || !b || !y || !ws) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -397,7 +398,7 @@ struct LossOps {
     a.latent = latent; a.W = W; a.bias = b; a.y = y;
     a.musd = (float*)(base + Lo.musd); a.part = (double*)(base + Lo.part); a.slab = (float*)(base + Lo.slab);
     a.dlatent = dlatent; a.grad = grad;
-    a.T = T; a.S = S; a.B = B;
+    a.T = T; a.S = S; a.B = B; a.dl_sir = dl_sir;
     const int lds = D::lds_bytes(S);
     if (!bwd) {
       if (!out) return UDE_E_INVALID;
@@ -424,6 +425,10 @@ struct LossOps {
                       const float* grad, void* ws, float* dlatent, float* dW, float* db, hipStream_t s) {
     return run(true, T, S, B, latent, W, b, y, grad, ws, nullptr, dlatent, dW, db, s);
   }
+  static int backward_sir(int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
+                          const float* grad, void* ws, float* dlat_sir, float* dW, float* db, hipStream_t s) {
+    return run(true, T, S, B, latent, W, b, y, grad, ws, nullptr, dlat_sir, dW, db, s, 1);
+  }
 };
 
 struct Entry {
@@ -434,7 +439,7 @@ struct Entry {
                     const float* const*, const float*, float*, hipStream_t);
   int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*, float*, hipStream_t);
   int (*backward)(const UdeProblem*, const float*, const void*, const float*, const float*, const float*,
-                  const float*, const float*, float*, float*, float*, hipStream_t);
+                  const float*, const float*, const float*, float*, float*, float*, hipStream_t);
   int (*dopri5_workspace)(const UdeProblem*, int, int64_t*);
   int (*dopri5_forward)(const UdeProblem*, const float*, const double*, double, double, double, int, const float*,
                         float*, void*, float*, UdeDopriInfo*, hipStream_t);
@@ -443,13 +448,15 @@ struct Entry {
                       hipStream_t);
   int (*loss_backward)(int, int, int, const float*, const float*, const float*, const float*, const float*, void*,
                        float*, float*, float*, hipStream_t);
+  int (*loss_backward_sir)(int, int, int, const float*, const float*, const float*, const float*, const float*,
+                           void*, float*, float*, float*, hipStream_t);
 };
 
 template <class M>
 constexpr Entry make_entry() {
   return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward,
                &DopriOps<M>::workspace, &DopriOps<M>::forward, &LossOps<M>::workspace, &LossOps<M>::forward,
-               &LossOps<M>::backward};
+               &LossOps<M>::backward, &LossOps<M>::backward_sir};
 }
 
 

@@ -64,11 +64,13 @@ struct KArgs {
   unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
   float* g0buf;               // backward: per-trajectory layer-0 gradient sums [tile][K0][16]
   const float* eslab;         // BAYES backward: the eps stream in slab order, [eval][SLAB_TOTAL]
+  const float* dlat_sir;      // backward: optional compact S, I, R cotangent (T, N, R, 3), added to
+                              // dlatent (which may then be null: all its entries zero)
 };
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
-constexpr int NPROF = 16;
+constexpr int NPROF = 20;
 struct Prof {
   unsigned long long acc[NPROF];
   unsigned long long last;
@@ -162,10 +164,13 @@ __device__ __forceinline__ f4 mma_frags(const f4* fr, const float* bp, int lane,
   return acc;
 }
 
-// ELU (alpha 1).  expm1 is evaluated unconditionally on min(x, 0) and selected,
-// so the compiler emits straight-line code instead of a divergent branch per value.
+// ELU (alpha 1) for x <= 0: exp(x) - 1 on the hardware exp2 (v_exp_f32, 1 ulp): 3 vector
+// instructions instead of the ~24 of the libm expm1f, whose cost paced every hidden-layer
+// epilogue at one wave per SIMD.  Absolute error <= ~1.3e-7 (the rounding of a value near 1;
+// torch's expm1 is more accurate only relative to tiny |x|, far below the parity bars).
+// Evaluated unconditionally on min(x, 0) and selected: straight-line code, no branch.
 __device__ __forceinline__ float elu1(float x) {
-  const float e = expm1f(fminf(x, 0.f));
+  const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.4426950408889634f) - 1.0f;
   return x > 0.f ? x : e;
 }
 
@@ -786,16 +791,19 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
 template <class M>
 __device__ __forceinline__ void out_load(const KArgs& A, const Sched& sc, int o, int n0,
                                          float (&gv)[M::SLOTS][3]) {
-  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
-  const float* gl = A.dlatent + (size_t)sc.out_j[o] * NRL;
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L, NR3 = (size_t)A.n_traj * M::R * 3;
+  const int jo = sc.out_j[o];
+  const float* gl = A.dlatent ? A.dlatent + (size_t)jo * NRL : nullptr;
+  const float* g3 = A.dlat_sir ? A.dlat_sir + (size_t)jo * NR3 : nullptr;
   sfor<M::SLOTS>([&](auto ss) {
     constexpr int sl = decltype(ss)::value;
     const int p = threadIdx.x + sl * NTHREADS;
     const int r = p / TT, t = p - r * TT, n = n0 + t;
     const bool valid = p < M::PAIRS && n < A.n_traj;
-    const size_t base = valid ? ((size_t)n * M::R + r) * M::L : 0;
+    const size_t nr = valid ? (size_t)n * M::R + r : 0;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) gv[sl][c] = valid ? gl[base + c] : 0.f;
+    for (int c = 0; c < 3; ++c)
+      gv[sl][c] = valid ? (gl ? gl[nr * M::L + c] : 0.f) + (g3 ? g3[nr * 3 + c] : 0.f) : 0.f;
   });
 }
 template <class M>
@@ -1145,6 +1153,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // every record access is a 16-B LDS op.
         if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
         flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        UDE_STAMP(pf, 16);
         if (next_out) {
           out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
@@ -1162,6 +1171,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
             }
           });
         }
+        UDE_STAMP(pf, 17);
         if (have_next) {
           sfor<SL>([&](auto ss) {
             constexpr int sl = decltype(ss)::value;
@@ -1173,6 +1183,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
             }
           });
         }
+        UDE_STAMP(pf, 18);
         // zero the padded rows of the final-layer gradient slots
         if constexpr (M::HAS_P) {
           constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
@@ -1246,7 +1257,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       if (n < A.n_traj) {
         const size_t base = ((size_t)n * M::R + r) * M::L;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] + A.dlatent[base + c];
+        for (int c = 0; c < 3; ++c)
+          A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] + (A.dlatent ? A.dlatent[base + c] : 0.f) +
+                            (A.dlat_sir ? A.dlat_sir[((size_t)n * M::R + r) * 3 + c] : 0.f);
       }
     }
     if constexpr (M::FULL0) {
@@ -1261,8 +1274,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
           const size_t base = ((size_t)n * M::R + r) * M::L + c;
           float v = lds[t * SR + M::DYS_OFF + s];
-          #pragma unroll 4
-          for (int jt = 0; jt <= A.n_out; ++jt) v += A.dlatent[(size_t)jt * NRL + base];
+          if (A.dlatent) {
+            #pragma unroll 4
+            for (int jt = 0; jt <= A.n_out; ++jt) v += A.dlatent[(size_t)jt * NRL + base];
+          }
           A.dy0[base] = v;
         }
       }
@@ -1605,7 +1620,10 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
   const int tile = blockIdx.x;
   const size_t NRL = (size_t)n_traj * M::R * M::L;
-  {
+  if (!dlatent) {                                    // static cotangents all zero
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < BLK; i += 256) tsum[i] = 0.f;
+  } else {
     const int nvalid = min(TT, n_traj - tile * TT) * M::R * M::L;
     const float* blk = dlatent + (size_t)tile * BLK;
     if constexpr ((M::R * M::L) % 4 == 0) {

@@ -45,9 +45,10 @@ struct LArgs {
   float* musd;           // (T, B, R, 2)   per-group mean / std of the predictions
   double* part;          // [grid][2]     nll / reg partial sums
   float* slab;           // [grid][SLAB]  dW / db partials (backward)
-  float* dlatent;        // (T, S*B, R, L) (backward)
+  float* dlatent;        // (T, S*B, R, L) (backward), or (T, S*B, R, 3) when dl_sir
   const float* grad;     // device [g_nll, g_reg] (backward)
   int T, S, B;
+  int dl_sir;            // backward writes only the S, I, R cotangents (the rest are zero)
 };
 
 // barrier for LDS hand-offs only: in-flight global loads (the next group's prefetch)
@@ -261,8 +262,16 @@ __device__ void loss_body(const LArgs& A, float* lds) {
         }
       }
       lds_barrier();
-      // ---- whole rows of d latent (static dims 0) with 16-B stores ---------------------
-      if constexpr ((D::R * L) % 4 == 0) {
+      // ---- d latent rows: compact S, I, R cotangents (handed to the solve's backward) ----
+      if (A.dl_sir) {
+        constexpr int R3 = 3 * D::R;
+        #pragma unroll 4
+        for (int i = tid; i < S * R3; i += LTHREADS) {
+          const int s = i / R3, e = i - s * R3;
+          A.dlatent[((size_t)t * N + (size_t)(s * A.B + b)) * R3 + e] = X[s * D::XS + e];
+        }
+      // ---- or whole rows of d latent (static dims 0) with 16-B stores -------------------
+      } else if constexpr ((D::R * L) % 4 == 0) {
         constexpr int RL4 = D::R * L / 4;
 #pragma unroll 4
         for (int i = tid; i < S * RL4; i += LTHREADS) {

@@ -66,8 +66,19 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
                      const float* dstats, float* dy0, float* grad_slab, float* dparams, ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || !dlatent) return UDE_E_INVALID;
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, nullptr, stats_out, dstats, dy0, grad_slab, dparams,
+                     (hipStream_t)stream);
+}
+
+int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                         const float* y0, const float* ckpt, const float* dlatent, const float* dlatent_sir,
+                         const float* stats_out, const float* dstats, float* dy0, float* grad_slab, float* dparams,
+                         ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
   if (!p || p->n_traj < 1 || p->n_steps < 0) return UDE_E_INVALID;
-  return e->backward(p, pack, sched, y0, ckpt, dlatent, stats_out, dstats, dy0, grad_slab, dparams,
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, dlatent_sir, stats_out, dstats, dy0, grad_slab, dparams,
                      (hipStream_t)stream);
 }
 
@@ -108,6 +119,15 @@ int ude_loss_head_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t 
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
   return e->loss_backward(T, S, B, latent, W, b, y, grad, ws, dlatent, dW, db, (hipStream_t)stream);
+}
+
+int ude_loss_head_backward_sir(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                               const float* W, const float* b, const float* y, const float* grad, void* ws,
+                               float* dlatent_sir, float* dW, float* db, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!dlatent_sir) return UDE_E_INVALID;
+  return e->loss_backward_sir(T, S, B, latent, W, b, y, grad, ws, dlatent_sir, dW, db, (hipStream_t)stream);
 }
 
 #ifdef UDE_PROFILE

@@ -36,9 +36,9 @@ _ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "i
          UDE_E_HIP: "HIP runtime error", UDE_E_SOLVER: "adaptive solve failed"}
 
 EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_weights_bayes",
-                    "ude_rk4_forward", "ude_rk4_backward", "ude_dopri5_workspace", "ude_dopri5_forward",
-                    "ude_loss_head_workspace", "ude_loss_head_forward", "ude_loss_head_backward",
-                    "ude_build_info")
+                    "ude_rk4_forward", "ude_rk4_backward", "ude_rk4_backward_sir", "ude_dopri5_workspace",
+                    "ude_dopri5_forward", "ude_loss_head_workspace", "ude_loss_head_forward",
+                    "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_build_info")
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -112,6 +112,8 @@ class NativeLib:
         L.ude_rk4_forward.restype = i32
         L.ude_rk4_backward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_rk4_backward.restype = i32
+        L.ude_rk4_backward_sir.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_rk4_backward_sir.restype = i32
         L.ude_dopri5_workspace.argtypes = [pdesc, pprob, i32, ctypes.POINTER(ctypes.c_int64)]
         L.ude_dopri5_workspace.restype = i32
         dbl = ctypes.c_double
@@ -124,6 +126,8 @@ class NativeLib:
         L.ude_loss_head_forward.restype = i32
         L.ude_loss_head_backward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_loss_head_backward.restype = i32
+        L.ude_loss_head_backward_sir.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_loss_head_backward_sir.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -158,6 +162,12 @@ class NativeLib:
         check(self.lib.ude_rk4_backward(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
                                         stats_out, dstats, dy0, slab, dparams, stream), "ude_rk4_backward")
 
+    def backward_sir(self, desc, prob, pack, sched, y0, ckpt, dlatent, dlat_sir, stats_out, dstats, dy0, slab,
+                     dparams, stream) -> None:
+        check(self.lib.ude_rk4_backward_sir(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
+                                            dlat_sir, stats_out, dstats, dy0, slab, dparams, stream),
+              "ude_rk4_backward_sir")
+
     def dopri5_workspace(self, desc, prob, device: int) -> int:
         out = ctypes.c_int64(0)
         check(self.lib.ude_dopri5_workspace(ctypes.byref(desc), ctypes.byref(prob), int(device), ctypes.byref(out)),
@@ -190,6 +200,10 @@ class NativeLib:
     def loss_backward(self, desc, T, S, B, latent, W, b, y, grad, ws, dlat, dW, db, stream) -> None:
         check(self.lib.ude_loss_head_backward(ctypes.byref(desc), int(T), int(S), int(B), latent, W, b, y, grad,
                                               ws, dlat, dW, db, stream), "ude_loss_head_backward")
+
+    def loss_backward_sir(self, desc, T, S, B, latent, W, b, y, grad, ws, dlat_sir, dW, db, stream) -> None:
+        check(self.lib.ude_loss_head_backward_sir(ctypes.byref(desc), int(T), int(S), int(B), latent, W, b, y, grad,
+                                                  ws, dlat_sir, dW, db, stream), "ude_loss_head_backward_sir")
 
     def build_info(self) -> str:
         return self.lib.ude_build_info().decode()
@@ -268,8 +282,9 @@ def prebuilt() -> NativeLib:
 
 def jit_library(cfg: _cfgs.Config) -> NativeLib:
     key = _cfgs.config_key(cfg)
-    h = hashlib.sha1(b"".join(open(os.path.join(CSRC, f), "rb").read()
-                              for f in ("ude_kernels.h", "ude_model.h", "ude_entry.h", "ude_rk4.hip"))).hexdigest()[:10]
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
+    srcs.append(os.path.join(INCLUDE, "ude_rk4.h"))
+    h = hashlib.sha1(b"".join(open(f, "rb").read() for f in srcs)).hexdigest()[:10]
     path = os.path.join(JIT_DIR, f"libude_rk4_{key}_{h}.so")
     if not os.path.exists(path):
         os.makedirs(JIT_DIR, exist_ok=True)

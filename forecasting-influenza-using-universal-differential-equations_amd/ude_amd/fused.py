@@ -62,9 +62,42 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class SirSink:
+    """Compact S, I, R cotangents of a fused solve's latent, deposited by consumers that read
+    only latent[..., :3] (the fused loss head, ude_amd/loss_head.py) in place of a full-size
+    (T, N, R, L) gradient that would be 5/8 zeros at L = 8.  A consumer that
+    deposits returns ZERO_GRAD-like stride-0 zeros for the latent itself, so the solve's backward
+    still runs; it adds the deposit to whatever full gradient other consumers produced."""
+
+    def __init__(self):
+        self.dl3 = None
+
+    def add(self, dl3: torch.Tensor) -> None:
+        self.dl3 = dl3 if self.dl3 is None else self.dl3 + dl3
+
+
+_ZEROS = {}
+
+
+def zero_grad_like(t: torch.Tensor) -> torch.Tensor:
+    """A stride-0 zero tensor of t's shape (no memory): the placeholder gradient of a latent
+    whose real cotangent went to its SirSink."""
+    key = (str(t.device), t.dtype)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros((), dtype=t.dtype, device=t.device)
+    return z.expand(t.shape)
+
+
+def _is_placeholder(g: torch.Tensor) -> bool:
+    z = _ZEROS.get((str(g.device), g.dtype))
+    return z is not None and g.data_ptr() == z.data_ptr() and all(st == 0 for st in g.stride())
+
+
 class FusedRK4(torch.autograd.Function):
     """Returns (latent, stats, ckpt); ckpt (the stage inputs of every step) is only a real
-    output when keep_ckpt is set (materialised tracking), else an empty tensor."""
+    output when keep_ckpt is set (materialised tracking), else an empty tensor.  latent carries
+    a SirSink (``latent._ude_sir_sink``) for compact S, I, R cotangents."""
 
     @staticmethod
     def forward(ctx, plan: Plan, y0: torch.Tensor, keep_ckpt: bool, *params: torch.Tensor):
@@ -88,10 +121,13 @@ class FusedRK4(torch.autograd.Function):
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
         ctx.plan = plan
+        ctx.sink = SirSink()
+        ctx.set_materialize_grads(False)
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(out_ck)
+        latent._ude_sir_sink = ctx.sink
         return latent, stats, out_ck
 
     @staticmethod
@@ -100,18 +136,22 @@ class FusedRK4(torch.autograd.Function):
         y0, pack, ckpt, stats = ctx.saved_tensors
         dev = y0.device
         stream = _stream(dev)
-        if dlatent is None:
+        dl3, ctx.sink.dl3 = ctx.sink.dl3, None
+        if dlatent is not None and _is_placeholder(dlatent):
+            dlatent = None                          # every consumer deposited compactly
+        if dlatent is None and dl3 is None:
             dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
-        dlatent = dlatent.contiguous().to(torch.float32)
+        if dlatent is not None:
+            dlatent = dlatent.contiguous().to(torch.float32)
         dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
         dy0 = torch.empty_like(y0)
         slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
         dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
-        plan.lib.backward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                          ckpt.data_ptr(), dlatent.data_ptr(), stats.data_ptr(), dstats.data_ptr(),
-                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                              ckpt.data_ptr(), _ptr(dlatent), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
+                              dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         return (None, dy0, None) + tuple(_split(dparams, plan.param_shapes))

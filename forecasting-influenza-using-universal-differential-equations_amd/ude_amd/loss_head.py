@@ -36,6 +36,8 @@ class _LossHead(torch.autograd.Function):
         if _fused.EVENTS is not None:
             e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_fwd", e0, e1))
         ctx.meta = (lib, desc, T, S, B)
+        # a latent straight from the fused solve takes its (S, I, R-only) cotangent compactly
+        ctx.sink = getattr(latent, "_ude_sir_sink", None) if COMPACT else None
         ctx.save_for_backward(latent, W, b, y, ws)
         ctx.mark_non_differentiable(ws)
         # ws starts with the per-(t, b, r) sample mean / std of the predictions ((T, B, R, 2))
@@ -46,28 +48,40 @@ class _LossHead(torch.autograd.Function):
         lib, desc, T, S, B = ctx.meta
         latent, W, b, y, ws = ctx.saved_tensors
         with torch.cuda.device(latent.device):
-            return _LossHead._backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg)
+            return _LossHead._backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, ctx.sink)
 
     @staticmethod
-    def _backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg):
+    def _backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, sink):
         dev = latent.device
         zero = torch.zeros((), dtype=torch.float32, device=dev)
         grad = torch.stack([zero if g_nll is None else g_nll.float().reshape(()),
                             zero if g_reg is None else g_reg.float().reshape(())])
-        dlat = torch.empty_like(latent)
         dW = torch.empty_like(W)
         db = torch.empty_like(b)
         if _fused.EVENTS is not None:
             e0 = _fused._ev(dev); e0.record()
-        lib.loss_backward(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
-                          grad.data_ptr(), ws.data_ptr(), dlat.data_ptr(), dW.data_ptr(), db.data_ptr(),
-                          _fused._stream(dev))
+        if sink is not None:
+            N, R = latent.shape[1], latent.shape[2]
+            dl3 = torch.empty((T, N, R, 3), dtype=torch.float32, device=dev)
+            lib.loss_backward_sir(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                  grad.data_ptr(), ws.data_ptr(), dl3.data_ptr(), dW.data_ptr(), db.data_ptr(),
+                                  _fused._stream(dev))
+            sink.add(dl3)
+            dlat = _fused.zero_grad_like(latent)
+        else:
+            dlat = torch.empty_like(latent)
+            lib.loss_backward(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
+                              grad.data_ptr(), ws.data_ptr(), dlat.data_ptr(), dW.data_ptr(), db.data_ptr(),
+                              _fused._stream(dev))
         if _fused.EVENTS is not None:
             e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_bwd", e0, e1))
         return None, None, None, None, None, dlat, dW, db, None
 
 
 _FITS = {}
+# hand the S, I, R cotangent to the fused solve's backward compactly (fused.SirSink) when the
+# latent comes straight from it; False: always write the full (T, N, R, L) d latent
+COMPACT = True
 
 
 def _fits(cfg, T: int, S: int, B: int, device: torch.device) -> bool:

@@ -133,6 +133,18 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
                      const float* dlatent, const float* stats_out, const float* dstats,
                      float* dy0, float* grad_slab, float* dparams, ude_stream_t stream);
 
+/* Backward with the S, I, R output cotangents handed over compactly: the
+ * training loss terms read only latent[..., :3] (lib/VAE.py:138, :189 -- Decoder and
+ * latent_init_loss), so their cotangent has zeros in every dim >= 3.  dlatent_sir: (T, N, R, 3)
+ * (nullable), added to dlatent (T, N, R, L) (nullable: all zero); with the fused loss head
+ * (ude_loss_head_backward_sir) neither the zero dims nor a full-size cotangent are written or
+ * read.  Replaces the same autograd backward as ude_rk4_backward (lib/VAE.py:203). */
+int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
+                         const void* sched, const float* y0, const float* ckpt,
+                         const float* dlatent, const float* dlatent_sir, const float* stats_out,
+                         const float* dstats, float* dy0, float* grad_slab, float* dparams,
+                         ude_stream_t stream);
+
 /* ---- adaptive Dormand-Prince solve (forward) ---------------------------------
  * Replaces torchdiffeq.odeint(func, y0, t, rtol, atol, method='dopri5',
  * options={'first_step': h?}) -- the default method of the solver API the
@@ -180,6 +192,13 @@ int ude_loss_head_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B
 int ude_loss_head_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
                            const float* W, const float* b, const float* y, const float* grad, void* ws,
                            float* dlatent, float* dW, float* db, ude_stream_t stream);
+
+/* As ude_loss_head_backward, but d latent is written compactly: dlatent_sir (T, S*B, R, 3) =
+ * the S, I, R cotangents (the loss terms do not read dims >= 3), to be handed to
+ * ude_rk4_backward_sir. */
+int ude_loss_head_backward_sir(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
+                               const float* W, const float* b, const float* y, const float* grad, void* ws,
+                               float* dlatent_sir, float* dW, float* db, ude_stream_t stream);
 
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);

@@ -119,3 +119,25 @@ def test_vae_calc_loss_large_sample_count_runs_eager(pkg, monkeypatch):
     """n_samples = 129 (> the kernel's 128 tile): calc_loss takes the reference's ops, no error."""
     took_fused, loss, grads = _vae_step(129, True, monkeypatch)
     assert not took_fused and torch.isfinite(loss)
+
+
+@pytest.mark.gpu
+def test_compact_sir_cotangent_matches_full(pkg, monkeypatch):
+    """the fused loss head hands the solve's backward only the S, I, R
+    cotangents (ude_loss_head_backward_sir -> ude_rk4_backward_sir) instead of a full
+    (T, N, R, L) d latent that is 5/8 zeros.  Same step with the hand-off disabled: identical
+    loss and bit-identical gradients (the compact path adds the same values in the same order)."""
+    from ude_amd import fused, loss_head
+    calls = []
+    real = fused.SirSink.add
+    monkeypatch.setattr(fused.SirSink, "add", lambda self, dl3: (calls.append(tuple(dl3.shape)), real(self, dl3)))
+    f1, loss_c, g_c = _vae_step(64, True, monkeypatch)
+    assert calls and calls[0][-1] == 3, calls
+    calls.clear()
+    monkeypatch.setattr(loss_head, "COMPACT", False)
+    monkeypatch.setattr(fused.SirSink, "add", lambda self, dl3: (calls.append(tuple(dl3.shape)), real(self, dl3)))
+    f2, loss_f, g_f = _vae_step(64, True, monkeypatch)
+    assert f1 and f2 and not calls
+    assert torch.equal(loss_c, loss_f)
+    for k in g_f:
+        assert torch.equal(g_c[k], g_f[k]), (k, normwise_rel(g_c[k], g_f[k]))

@@ -12,6 +12,8 @@ tail -c 1500 gpurun_out/bench.json
 if [ "$1" = "prof" ]; then
   timeout -k 10 120 python -u tools/stage_profile.py us_northstar > gpurun_out/stage_m1.txt 2>&1 || exit $?
   cat gpurun_out/stage_m1.txt
+  timeout -k 10 120 python -u tools/stage_profile.py state49 > gpurun_out/stage_s49.txt 2>&1 || exit $?
+  cat gpurun_out/stage_s49.txt
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_m1 -o m1 -- python3 bench.py --workload us_northstar --steps 5 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/prof_m1.log 2>&1 || exit $?
 fi
 exit $rc

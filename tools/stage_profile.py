@@ -19,8 +19,11 @@ from ude_amd import _native  # noqa: E402
 import bench  # noqa: E402
 
 SEG = {0: "stage input (ckpt)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1", 4: "fwd d2", 5: "fwd d3",
-       6: "flux bwd", 11: "barrier after flux", 10: "bwd d3", 9: "bwd d2", 8: "bwd d1", 7: "bwd d0",
-       12: "RK adjoint", 13: "step end (RK_A)", 14: "step start (cotangents)", 15: "tile start/end"}
+       16: "flux bwd", 17: "  output cotangents", 18: "  stage input staging", 6: "  zero padded rows",
+       11: "barrier after flux", 10: "bwd d3", 9: "bwd d2", 8: "bwd d1", 7: "bwd d0",
+       12: "RK adjoint / split-x0 sum", 13: "step end (RK_A)", 14: "step start (cotangents)", 15: "tile start/end"}
+ORDER = [15, 14, 0, 1, 2, 3, 4, 5, 16, 17, 18, 6, 11, 10, 9, 8, 7, 12, 13]
+NPROF = 20
 
 
 def main():
@@ -40,19 +43,19 @@ def main():
     mod, y0, t, dlat = bench.build(pkg, w, dev, seed=1)
     from ude_amd import distributed as udist
     bench.one_step(pkg, udist, mod, y0, t, dlat, 1)        # warm up (grid size known after)
-    buf = torch.zeros(4096 * 16, dtype=torch.int64, device=dev)
+    buf = torch.zeros(4096 * NPROF, dtype=torch.int64, device=dev)
     lib.lib.ude_debug_set_prof(buf.data_ptr())
     bench.one_step(pkg, udist, mod, y0, t, dlat, 1)
     torch.cuda.synchronize()
     lib.lib.ude_debug_set_prof(None)
-    v = buf.view(-1, 16).double()
+    v = buf.view(-1, NPROF).double()
     used = v[v.sum(1) > 0]
     tiles = (w["n_traj"] + 15) // 16
     stages = tiles * 4 * (len(t) - 1) / used.shape[0]
     per = used.mean(0) / stages
     tot = float(per.sum())
     print(f"workgroups {used.shape[0]}, stages per WG {stages:.1f}, cycles per stage {tot:.0f}")
-    for k in sorted(SEG, key=lambda s: [15, 14, 0, 1, 2, 3, 4, 5, 6, 11, 10, 9, 8, 7, 12, 13].index(s)):
+    for k in ORDER:
         print(f"  {SEG[k]:24s} {float(per[k]):9.0f}  {100 * float(per[k]) / tot:5.1f}%")
 
 

@@ -19,4 +19,5 @@ const Entry UDE_CAT(ude_entry_, UDE_CFG_ID) = make_entry<UDE_MODEL_X(UDE_ONE_CON
 template struct ude::Ops<UDE_MODEL_X(UDE_ONE_CONFIG)>;
 template struct ude::DopriOps<UDE_MODEL_X(UDE_ONE_CONFIG)>;
 template struct ude::LossOps<UDE_MODEL_X(UDE_ONE_CONFIG)>;
+template struct ude::EvalOps<UDE_MODEL_X(UDE_ONE_CONFIG)>;
 #endif

@@ -7,6 +7,7 @@
 #include "ude_kernels.h"
 #include "ude_dopri5.h"
 #include "ude_loss.h"
+#include "ude_eval.h"
 
 namespace ude {
 
@@ -34,13 +35,28 @@ bool matches(const UdeModelDesc* d) {
 template <class M>
 struct Ops {
   static constexpr int DY0_STATIC_LDS = TT * M::R * M::L * 4;
+  static constexpr int LDS_MAX = 160 * 1024;
+  static int64_t sched_bytes(const UdeProblem* p) {
+    return (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
+  }
+  // bytes of schedule copied into LDS behind a record of rec bytes: all of it when that does
+  // not lower the kernel's occupancy, else 0 (read from global memory)
+  static int sched_lds(const void* kern, int rec, const UdeProblem* p) {
+    const int64_t sb = (sched_bytes(p) + 15) & ~(int64_t)15;
+    if (sb == 0 || rec + sb > LDS_MAX) return 0;
+    int o0 = 0, o1 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, kern, NTHREADS, rec) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, kern, NTHREADS, (size_t)(rec + sb)) != hipSuccess) return 0;
+    return o1 >= o0 ? (int)sb : 0;
+  }
   static_assert(!M::HOIST || DY0_STATIC_LDS <= 160 * 1024, "dy0 static time sums do not fit the 160 KiB LDS");
   static int ensure_attrs() {
     static bool done = false;
     if (done) return UDE_OK;
-    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
-    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
-    HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_B));
+    // record + (when it fits) the schedule: up to the full 160 KiB
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
     // the static-feature dy0 kernel stages one tile's (16, R, L) time sums of d latent in LDS
     if (M::HOIST)
       HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -86,7 +102,7 @@ struct Ops {
     const int64_t ne = n_evals(p) > 0 ? n_evals(p) : 1;
     // BAYES: [eval][PACK_TOTAL] weight samples, then [eval][SLAB_TOTAL] eps in slab order
     o->pack_bytes = M::BAYES ? ne * (int64_t)(M::PACK_TOTAL + M::SLAB_TOTAL) * 4 : (int64_t)M::PACK_TOTAL * 4;
-    o->sched_bytes = (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
+    o->sched_bytes = sched_bytes(p);
     o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * M::F * TT * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
     o->grad_slab_bytes = (int64_t)gb * M::SLAB_STRIDE * 4 + static_ws_floats(n_tiles) * 4;
@@ -169,8 +185,10 @@ struct Ops {
     a.latent = latent; a.ckpt = ckpt; a.stats_slab = stats_slab;
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
-    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
-    else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    const void* kf = ckpt ? (const void*)&ude_fwd_kernel<M, true> : (const void*)&ude_fwd_kernel<M, false>;
+    a.sched_lds = sched_lds(kf, M::LDS_F, p);
+    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F + a.sched_lds, s, a);
+    else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F + a.sched_lds, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
     hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
@@ -203,7 +221,8 @@ struct Ops {
 #endif
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
-    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
+    a.sched_lds = sched_lds((const void*)&ude_bwd_kernel<M>, M::LDS_B, p);
+    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B + a.sched_lds, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
@@ -431,6 +450,104 @@ struct LossOps {
   }
 };
 
+// ---- one RHS evaluation + its VJP (ude_eval.h) -------------------------------------------
+template <class M>
+struct EvalOps {
+  static int grids(int device, int n_tiles, int* gf, int* gb) {
+    if constexpr (M::BAYES) {
+      return UDE_E_UNSUPPORTED;
+    } else {
+    static bool done = false;
+    if (!done) {
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_eval_fwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_eval_vjp_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_B));
+      if (M::HOIST)
+        HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   TT * M::R * M::L * 4));
+      done = true;
+    }
+    int cus = 0, of = 0, ob = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, (const void*)&ude_eval_fwd_kernel<M>, NTHREADS, M::LDS_F));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_eval_vjp_kernel<M>, NTHREADS, M::LDS_B));
+    const long mf = (long)cus * (of < 1 ? 1 : of), mb = (long)cus * (ob < 1 ? 1 : ob);
+    *gf = (int)(n_tiles < mf ? n_tiles : mf);
+    *gb = (int)(n_tiles < mb ? n_tiles : mb);
+    return UDE_OK;
+    }
+  }
+  static int workspace(const UdeProblem* p, int device, int64_t* bytes) {
+    if (M::BAYES) return UDE_E_UNSUPPORTED;      // each evaluation's sample is a deterministic RHS
+    if (p->n_traj < 1) return UDE_E_INVALID;
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(device, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    *bytes = ((int64_t)gb * M::SLAB_STRIDE + Ops<M>::static_ws_floats(n_tiles)) * 4;
+    return UDE_OK;
+  }
+  static int forward(const UdeProblem* p, const float* pack, const float* x, float* f, float* rates, float* fa,
+                     hipStream_t s) {
+    if constexpr (M::BAYES) {
+      return UDE_E_UNSUPPORTED;
+    } else {
+    if (!pack || !x || !f || p->n_traj < 1) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(dev, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    EArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.x = x; a.f = f; a.rates = rates; a.fa = fa;
+    a.n_traj = p->n_traj; a.n_tiles = n_tiles; a.fa_w = p->fa_w;
+    hipLaunchKernelGGL((ude_eval_fwd_kernel<M>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+    }
+  }
+  static int vjp(const UdeProblem* p, const float* pack, const float* x, const float* cot_f, const float* cot_rates,
+                 const float* cot_fa, float* dx, void* ws, float* dparams, hipStream_t s) {
+    if constexpr (M::BAYES) {
+      return UDE_E_UNSUPPORTED;
+    } else {
+    if (!pack || !x || !cot_f || !dx || !ws || !dparams || p->n_traj < 1) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(dev, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    float* slab = (float*)ws;
+    float* g0buf = slab + (size_t)gb * M::SLAB_STRIDE;
+    float* part = g0buf + (size_t)n_tiles * M::K0 * TT;
+    EArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.x = x; a.cot_f = cot_f; a.cot_rates = cot_rates; a.cot_fa = cot_fa;
+    a.dx = dx; a.slab = slab; a.g0buf = g0buf;
+    a.n_traj = p->n_traj; a.n_tiles = n_tiles; a.fa_w = p->fa_w;
+    hipLaunchKernelGGL((ude_eval_vjp_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
+                       (const float*)slab, gb, dparams);
+    HIPCHK(hipGetLastError());
+    if (M::HOIST) {
+      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS), dim3(256), 0, s,
+                         (const float*)g0buf, x, p->n_traj, n_tiles, part);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
+                         (const float*)part, dparams);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3(n_tiles), dim3(256), TT * M::R * M::L * 4, s,
+                         (const float*)g0buf, pack, (const float*)nullptr, p->n_traj, 0, dx);
+      HIPCHK(hipGetLastError());
+    }
+    return UDE_OK;
+    }
+  }
+};
+
 struct Entry {
   bool (*match)(const UdeModelDesc*);
   int (*query)(const UdeProblem*, int, UdeSizes*);
@@ -450,13 +567,18 @@ struct Entry {
                        float*, float*, float*, hipStream_t);
   int (*loss_backward_sir)(int, int, int, const float*, const float*, const float*, const float*, const float*,
                            void*, float*, float*, float*, hipStream_t);
+  int (*rhs_workspace)(const UdeProblem*, int, int64_t*);
+  int (*rhs_forward)(const UdeProblem*, const float*, const float*, float*, float*, float*, hipStream_t);
+  int (*rhs_vjp)(const UdeProblem*, const float*, const float*, const float*, const float*, const float*, float*,
+                 void*, float*, hipStream_t);
 };
 
 template <class M>
 constexpr Entry make_entry() {
   return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward,
                &DopriOps<M>::workspace, &DopriOps<M>::forward, &LossOps<M>::workspace, &LossOps<M>::forward,
-               &LossOps<M>::backward, &LossOps<M>::backward_sir};
+               &LossOps<M>::backward, &LossOps<M>::backward_sir, &EvalOps<M>::workspace, &EvalOps<M>::forward,
+               &EvalOps<M>::vjp};
 }
 
 

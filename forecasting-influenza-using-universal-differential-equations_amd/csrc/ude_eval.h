@@ -1,0 +1,323 @@
+// gfx950 kernels for ONE evaluation of the UDE right-hand side and its VJP:
+//   forward  f = RHS(x), rates = |net(x)|, Fa = aug_net(x)     (lib/models.py:129-146, :177-188,
+//            :230-254 -- the tensors forward() returns and appends to params / tracker)
+//   VJP      dx, dW given the cotangents of f, rates and Fa
+// for every trajectory of a batch, one tile of 16 trajectories per workgroup, on the same MFMA
+// layer machinery as the fused RK4 kernels (mlp_forward / mlp_backward, register-resident
+// weights, static-feature hoist).
+//
+// These serve every solve that is not the fused fixed-grid RK4: the RHS module's forward on
+// a HIP device (so eager solvers -- dopri5 with autograd, torchdiffeq's odeint_adjoint
+// backward, euler / midpoint -- call one kernel per evaluation instead of ~40 PyTorch ops),
+// and the Bayesian RHS at sizes whose two dW accumulator sets do not fit the fused kernel's
+// registers (models_bayes.py:43-48: each evaluation's sampled weights are a deterministic
+// RHS for that evaluation; d mean / d std follow from dW on the host).
+#pragma once
+#include "ude_kernels.h"
+
+namespace ude {
+
+struct EArgs {
+  const float* pack;
+  const float* x;          // (N, R, L) evaluation point
+  float* f;                // forward: (N, R, L) RHS value (dims >= 3 zero, masked)
+  float* rates;            // forward: (N, R, 2) |net(x)| (nullable)
+  float* fa;               // forward: (N, R, 3) aug_net(x) (nullable)
+  const float* cot_f;      // VJP: (N, R, L) cotangent of f (dims >= 3 ignored: f is 0 there)
+  const float* cot_rates;  // VJP: (N, R, 2) (nullable: zero)
+  const float* cot_fa;     // VJP: (N, R, 3) (nullable: zero)
+  float* dx;               // VJP: (N, R, L); static dims written by ude_dy0_static_kernel (HOIST)
+  float* slab;             // VJP: per-workgroup dW partials [grid][SLAB_STRIDE]
+  float* g0buf;            // VJP: per-trajectory layer-0 output gradients [tile][K0][16] (HOIST)
+  int n_traj, n_tiles;
+  float fa_w;
+};
+
+// ---- forward --------------------------------------------------------------------------
+template <class M, int W>
+__device__ void eval_fwd_body(const EArgs& A, float* lds) {
+  constexpr int SR = M::SR_F;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
+  WRegs<M, W, false> wr;
+  wr.load(rs, lane);
+  #pragma unroll 1
+  for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
+  __syncthreads();
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
+    #pragma unroll 1
+    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+      const int r = p / TT, t = p - r * TT, n = n0 + t;
+      const float* src = A.x + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = n < A.n_traj ? src[c] : 0.f;
+    }
+    load_static<M, SR, M::XSF_OFF>(A.x, lds, n0, A.n_traj);
+    __syncthreads();
+    f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
+    static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
+    __syncthreads();
+    mlp_forward<M, W, SR>(rs, lds, c1, lane, wr);
+    #pragma unroll 1
+    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+      const int r = p / TT, t = p - r * TT, n = n0 + t;
+      if (n >= A.n_traj) continue;
+      const float* rec = lds + t * SR;
+      float Y[3], f[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Y[c] = rec[M::Y_OFF + 3 * r + c];
+      if constexpr (M::HAS_P) {
+        const float b = fabsf(rec[M::act_off(0, M::nl(0) - 1) + 2 * r]);
+        const float gm = fabsf(rec[M::act_off(0, M::nl(0) - 1) + 2 * r + 1]);
+        const float plus = (b * Y[0]) * Y[1];
+        const float minus = gm * Y[1];
+        f[0] = -plus; f[1] = plus - minus; f[2] = minus;
+        if (A.rates) {
+          A.rates[((size_t)n * M::R + r) * 2] = b;
+          A.rates[((size_t)n * M::R + r) * 2 + 1] = gm;
+        }
+      }
+      if constexpr (M::HAS_A) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float v = rec[M::act_off(1, M::nl(1) - 1) + 3 * r + c];
+          if constexpr (M::HAS_P) f[c] = f[c] + A.fa_w * v;
+          else f[c] = v;
+          if (A.fa) A.fa[((size_t)n * M::R + r) * 3 + c] = v;
+        }
+      }
+      float* dst = A.f + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dst[c] = (Y[c] > 2.f || Y[c] < -1.f) ? 0.f : f[c];
+      for (int c = 3; c < M::L; ++c) dst[c] = 0.f;
+    }
+    __syncthreads();
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(NTHREADS, 2) void ude_eval_fwd_kernel(EArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w == 0) eval_fwd_body<M, 0>(a, lds);
+  else if (w == 1) eval_fwd_body<M, 1>(a, lds);
+  else if (w == 2) eval_fwd_body<M, 2>(a, lds);
+  else eval_fwd_body<M, 3>(a, lds);
+}
+
+// ---- VJP --------------------------------------------------------------------------------
+// Layer-0 input gradient epilogue: accumulates into the per-trajectory dx record (the RK_ACCY
+// slot of the backward record; dynamic rows only -- static rows go through G0, HOIST).
+template <class M, int SR>
+struct EvalEp {
+  float* rec;
+  __device__ __forceinline__ void operator()(int f0, f4 dY) const {
+    if (f0 >= M::F4) return;
+    *reinterpret_cast<f4*>(rec + M::RK_ACCY + f0) += dY;
+  }
+};
+
+// Flux backward of one evaluation: the cotangents of f (masked outside [-1, 2]), of rates
+// (through |.|) and of Fa -> final-layer gradients, and the direct d f / d (S, I) part of dx.
+// The tile's cotangents were staged in the record: f in RK_DK1, rates in RK_DK2 ([r][2]),
+// Fa in RK_DK3 ([r][3]).
+template <class M, int SR>
+__device__ __forceinline__ void eval_flux_backward(float* lds, const EArgs& A, int n0) {
+  constexpr int RG = (M::R + 3) / 4, ITEMS = TT * RG;
+  constexpr int QO = M::HAS_P ? M::act_off(0, M::nl(0) - 1) : 0, QG = M::HAS_P ? M::gbuf(0, M::nl(0) - 1) : 0;
+  constexpr int FO = M::HAS_A ? M::act_off(1, M::nl(1) - 1) : 0, FG = M::HAS_A ? M::gbuf(1, M::nl(1) - 1) : 0;
+  #pragma unroll 1
+  for (int it = threadIdx.x; it < ITEMS; it += NTHREADS) {
+    const int t = it & (TT - 1), rg = it >> 4;
+    const bool valid = n0 + t < A.n_traj;
+    float* rec = lds + t * SR;
+    float dyf[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) dyf[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * rg + j;
+      if (r >= M::R) break;
+      const bool live = valid;
+      float Y[3], dres[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        Y[c] = rec[M::Y_OFF + 3 * r + c];
+        const float dk = rec[M::RK_DK1 + 3 * r + c];
+        dres[c] = (!live || Y[c] > 2.f || Y[c] < -1.f) ? 0.f : dk;
+      }
+      if constexpr (M::HAS_A) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float d = M::HAS_P ? A.fa_w * dres[c] : dres[c];
+          rec[FG + 3 * r + c] = live ? d + rec[M::RK_DK3 + 3 * r + c] : 0.f;
+        }
+      }
+      if constexpr (M::HAS_P) {
+        const float q0 = rec[QO + 2 * r], q1 = rec[QO + 2 * r + 1];
+        const float b = fabsf(q0), gm = fabsf(q1);
+        const float dplus = dres[1] - dres[0];
+        const float dminus = dres[2] - dres[1];
+        const float dpi = dplus * Y[1];
+        float dbeta = dpi * Y[0];
+        float dgam = dminus * Y[1];
+        dyf[3 * j] = dpi * b;
+        dyf[3 * j + 1] = dplus * (b * Y[0]) + dminus * gm;
+        if (live) {
+          dbeta += rec[M::RK_DK2 + 2 * r];
+          dgam += rec[M::RK_DK2 + 2 * r + 1];
+        } else {
+          dbeta = 0.f; dgam = 0.f;
+        }
+        rec[QG + 2 * r] = q0 > 0.f ? dbeta : (q0 < 0.f ? -dbeta : 0.f);
+        rec[QG + 2 * r + 1] = q1 > 0.f ? dgam : (q1 < 0.f ? -dgam : 0.f);
+      }
+    }
+    // direct part of dx (the MLP part is added by the layer-0 epilogue)
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const f4 dY = {dyf[4 * v], dyf[4 * v + 1], dyf[4 * v + 2], dyf[4 * v + 3]};
+      *reinterpret_cast<f4*>(rec + M::RK_ACCY + 12 * rg + 4 * v) = dY;
+    }
+  }
+}
+
+template <class M, int W>
+__device__ void eval_vjp_body(const EArgs& A, float* lds) {
+  constexpr int SR = M::SR_B;
+  constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
+  constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int t16 = lane & 15, g = lane >> 4;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
+  const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
+  f4 dw[NDWn], dws[1], g0t[NZn], c1[NZn];
+#pragma unroll
+  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  WRegs<M, W, true> wr;
+  wr.load(rs, lane);
+  #pragma unroll 1
+  for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;
+  __syncthreads();
+
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
+    load_static<M, SR, M::XSB_OFF>(A.x, lds, n0, A.n_traj);
+    // evaluation point and the three cotangents -> record
+    #pragma unroll 1
+    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+      const int r = p / TT, t = p - r * TT, n = n0 + t;
+      const bool valid = n < A.n_traj;
+      const size_t nr = valid ? (size_t)n * M::R + r : 0;
+      float* rec = lds + t * SR;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        rec[M::Y_OFF + 3 * r + c] = valid ? A.x[nr * M::L + c] : 0.f;
+        rec[M::RK_DK1 + 3 * r + c] = valid ? A.cot_f[nr * M::L + c] : 0.f;
+        rec[M::RK_DK3 + 3 * r + c] = (valid && A.cot_fa) ? A.cot_fa[nr * 3 + c] : 0.f;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) rec[M::RK_DK2 + 2 * r + c] = (valid && A.cot_rates) ? A.cot_rates[nr * 2 + c] : 0.f;
+    }
+    __syncthreads();
+    static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    __syncthreads();
+    mlp_forward<M, W, SR>(rs, lds, c1, lane, wr);
+    eval_flux_backward<M, SR>(lds, A, n0);
+    // zero the padded rows of the final-layer gradient slots
+    if constexpr (M::HAS_P) {
+      constexpr int lo = 2 * M::R, hi = M::kout(0, M::nl(0) - 1);
+      #pragma unroll 1
+      for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
+        const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
+        lds[t * SR + M::gbuf(0, M::nl(0) - 1) + o] = 0.f;
+      }
+    }
+    if constexpr (M::HAS_A) {
+      constexpr int lo = 3 * M::R, hi = M::kout(1, M::nl(1) - 1);
+      #pragma unroll 1
+      for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
+        const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
+        lds[t * SR + M::gbuf(1, M::nl(1) - 1) + o] = 0.f;
+      }
+    }
+    __syncthreads();
+    mlp_backward<M, W, SR>(rs, rs, lds, dw, dws, g0t, lane, nullptr, EvalEp<M, SR>{lds + t16 * SR}, wr);
+    if constexpr (M::SPLITX0) {
+      constexpr int NVX = cmin(M::F4, M::F16) / 4;
+      #pragma unroll 1
+      for (int i = tid; i < TT * NVX; i += NTHREADS) {
+        const int t = i / NVX, v = i - t * NVX, f0 = 4 * v;
+        const int m = f0 >> 4, li = ((f0 >> 2) & 3) * 16 + t;
+        f4 s = f4zero();
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+          s += *reinterpret_cast<const f4*>(lds + M::X0P_LDS + ((w * M::XT(0) + m) * 64 + li) * 4);
+        EvalEp<M, SR>{lds + t * SR}(f0, s);
+      }
+    }
+    __syncthreads();
+    // dx (dynamic dims; static dims: ude_dy0_static_kernel from the G0 sums below)
+    #pragma unroll 1
+    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
+      const int r = p / TT, t = p - r * TT, n = n0 + t;
+      if (n < A.n_traj) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) A.dx[((size_t)n * M::R + r) * M::L + c] = lds[t * SR + M::RK_ACCY + 3 * r + c];
+      }
+    }
+    // per-trajectory layer-0 output gradients -> G0 (static-feature gradients) + bias row sums
+    sfor<M::FT(0)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(0, k) == W) {
+        const f4 gv = g0t[M::nz_before(W, k)];
+        if constexpr (M::HOIST) {
+          float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
+          dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
+        }
+        f4 r = gv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+        }
+        if (t16 == 0) {
+          float* db = lds + M::DB_LDS + k * 16 + g * 4;
+          db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+        }
+      }
+    });
+    __syncthreads();
+  }
+
+  sfor<M::D>([&](auto dd) {
+    constexpr int d = decltype(dd)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k);
+        sfor<M::rti(net, d)>([&](auto cc) {
+          constexpr int ct = decltype(cc)::value;
+          reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
+        });
+      }
+    });
+  });
+  #pragma unroll 1
+  for (int i = tid; i < M::NDB; i += NTHREADS) myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
+}
+
+template <class M>
+__global__ __launch_bounds__(NTHREADS) void ude_eval_vjp_kernel(EArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w == 0) eval_vjp_body<M, 0>(a, lds);
+  else if (w == 1) eval_vjp_body<M, 1>(a, lds);
+  else if (w == 2) eval_vjp_body<M, 2>(a, lds);
+  else eval_vjp_body<M, 3>(a, lds);
+}
+
+}  // namespace ude

@@ -60,12 +60,13 @@ struct KArgs {
   float* dy0;
   float* slab;
   int n_traj, n_steps, n_out, n_tiles;
+  int sched_lds;              // > 0: copy the schedule (this many bytes) into LDS after the record
   float fa_w;
   unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
   float* g0buf;               // backward: per-trajectory layer-0 gradient sums [tile][K0][16]
   const float* eslab;         // BAYES backward: the eps stream in slab order, [eval][SLAB_TOTAL]
-  const float* dlat_sir;      // backward: optional compact S, I, R cotangent (T, N, R, 3), added to
-                              // dlatent (which may then be null: all its entries zero)
+  const float* dlat_sir;      // backward: the compact S, I, R cotangent (T, N, R, 3) when dlatent is
+                              // null (its dims >= 3 all zero); exactly one of the two is set
 };
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
@@ -89,6 +90,19 @@ struct Prof {
 #else
 #define UDE_STAMP(pf, seg) do { } while (0)
 #endif
+
+// The step / output schedule is read every stage (dt, the output CSR): the launch copies it
+// into LDS behind the record when there is room (A.sched_lds), so those reads are LDS
+// round trips instead of dependent global loads on the stage's critical path.
+__device__ __forceinline__ const unsigned char* stage_sched(const KArgs& A, float* lds, int rec_bytes) {
+  if (A.sched_lds <= 0) return A.sched;
+  unsigned int* dst = reinterpret_cast<unsigned int*>(reinterpret_cast<unsigned char*>(lds) + rec_bytes);
+  const unsigned int* src = reinterpret_cast<const unsigned int*>(A.sched);
+  #pragma unroll 1
+  for (int i = threadIdx.x; i < A.sched_lds / 4; i += NTHREADS) dst[i] = src[i];
+  __syncthreads();
+  return reinterpret_cast<const unsigned char*>(dst);
+}
 
 struct Sched {
   const float* dt;
@@ -164,13 +178,13 @@ __device__ __forceinline__ f4 mma_frags(const f4* fr, const float* bp, int lane,
   return acc;
 }
 
-// ELU (alpha 1) for x <= 0: exp(x) - 1 on the hardware exp2 (v_exp_f32, 1 ulp): 3 vector
-// instructions instead of the ~24 of the libm expm1f, whose cost paced every hidden-layer
-// epilogue at one wave per SIMD.  Absolute error <= ~1.3e-7 (the rounding of a value near 1;
-// torch's expm1 is more accurate only relative to tiny |x|, far below the parity bars).
-// Evaluated unconditionally on min(x, 0) and selected: straight-line code, no branch.
+// ELU (alpha 1).  expm1 is evaluated unconditionally on min(x, 0) and selected,
+// so the compiler emits straight-line code instead of a divergent branch per value.
+// (libm expm1f: torch's expm1-grade accuracy; the adaptive dopri5 step control is
+// sensitive to the last bits of the RHS, measured: a 1-ulp-of-1 exp2 variant moves its
+// evaluation points enough to shift the side statistics by 2e-3.)
 __device__ __forceinline__ float elu1(float x) {
-  const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.4426950408889634f) - 1.0f;
+  const float e = expm1f(fminf(x, 0.f));
   return x > 0.f ? x : e;
 }
 
@@ -392,7 +406,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
   const int tid = threadIdx.x, lane = tid & 63;
-  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const Sched sc(stage_sched(A, lds, M::LDS_F), A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
   double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
@@ -791,19 +805,18 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
 template <class M>
 __device__ __forceinline__ void out_load(const KArgs& A, const Sched& sc, int o, int n0,
                                          float (&gv)[M::SLOTS][3]) {
-  const size_t NRL = (size_t)A.n_traj * M::R * M::L, NR3 = (size_t)A.n_traj * M::R * 3;
-  const int jo = sc.out_j[o];
-  const float* gl = A.dlatent ? A.dlatent + (size_t)jo * NRL : nullptr;
-  const float* g3 = A.dlat_sir ? A.dlat_sir + (size_t)jo * NR3 : nullptr;
+  // one source: the full (T, N, R, L) cotangent, or the compact S, I, R one (exactly one of
+  // them is set, see ude_rk4_backward_sir)
+  const int ld = A.dlatent ? M::L : 3;
+  const float* gl = (A.dlatent ? A.dlatent : A.dlat_sir) + (size_t)sc.out_j[o] * A.n_traj * M::R * ld;
   sfor<M::SLOTS>([&](auto ss) {
     constexpr int sl = decltype(ss)::value;
     const int p = threadIdx.x + sl * NTHREADS;
     const int r = p / TT, t = p - r * TT, n = n0 + t;
     const bool valid = p < M::PAIRS && n < A.n_traj;
-    const size_t nr = valid ? (size_t)n * M::R + r : 0;
+    const size_t base = valid ? ((size_t)n * M::R + r) * ld : 0;
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
-      gv[sl][c] = valid ? (gl ? gl[nr * M::L + c] : 0.f) + (g3 ? g3[nr * 3 + c] : 0.f) : 0.f;
+    for (int c = 0; c < 3; ++c) gv[sl][c] = valid ? gl[base + c] : 0.f;
   });
 }
 template <class M>
@@ -980,7 +993,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int t16 = lane & 15, g = lane >> 4;
-  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const Sched sc(stage_sched(A, lds, M::LDS_B), A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
@@ -1258,8 +1271,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         const size_t base = ((size_t)n * M::R + r) * M::L;
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] + (A.dlatent ? A.dlatent[base + c] : 0.f) +
-                            (A.dlat_sir ? A.dlat_sir[((size_t)n * M::R + r) * 3 + c] : 0.f);
+          A.dy0[base + c] = lds[t * SR + M::RK_A + 3 * r + c] +
+                            (A.dlatent ? A.dlatent[base + c] : A.dlat_sir[((size_t)n * M::R + r) * 3 + c]);
       }
     }
     if constexpr (M::FULL0) {

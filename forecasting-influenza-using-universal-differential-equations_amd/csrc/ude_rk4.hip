@@ -77,7 +77,7 @@ int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float
                          ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
-  if (!p || p->n_traj < 1 || p->n_steps < 0) return UDE_E_INVALID;
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || (!dlatent) == (!dlatent_sir)) return UDE_E_INVALID;
   return e->backward(p, pack, sched, y0, ckpt, dlatent, dlatent_sir, stats_out, dstats, dy0, grad_slab, dparams,
                      (hipStream_t)stream);
 }
@@ -128,6 +128,30 @@ int ude_loss_head_backward_sir(const UdeModelDesc* m, int32_t T, int32_t S, int3
   if (!e) return UDE_E_UNSUPPORTED;
   if (!dlatent_sir) return UDE_E_INVALID;
   return e->loss_backward_sir(T, S, B, latent, W, b, y, grad, ws, dlatent_sir, dW, db, (hipStream_t)stream);
+}
+
+int ude_rhs_workspace(const UdeModelDesc* m, const UdeProblem* p, int device, int64_t* ws_bytes) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || !ws_bytes) return UDE_E_INVALID;
+  return e->rhs_workspace(p, device, ws_bytes);
+}
+
+int ude_rhs_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x, float* f,
+                    float* rates, float* fa, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p) return UDE_E_INVALID;
+  return e->rhs_forward(p, pack, x, f, rates, fa, (hipStream_t)stream);
+}
+
+int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x, const float* cot_f,
+                const float* cot_rates, const float* cot_fa, float* dx, void* ws, float* dparams,
+                ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p) return UDE_E_INVALID;
+  return e->rhs_vjp(p, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, (hipStream_t)stream);
 }
 
 #ifdef UDE_PROFILE

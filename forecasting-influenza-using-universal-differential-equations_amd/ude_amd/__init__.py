@@ -4,6 +4,7 @@ behind the reference's own API (lib/models.py classes, torchdiffeq.odeint).
 """
 from .rhs import Fp, Fa, FaFp, UDE_CLASSES
 from .solvers import odeint, fusable
+from .adjoint import odeint_adjoint
 from . import _native, configs
 
-__all__ = ["Fp", "Fa", "FaFp", "odeint", "fusable", "UDE_CLASSES"]
+__all__ = ["Fp", "Fa", "FaFp", "odeint", "odeint_adjoint", "fusable", "UDE_CLASSES"]

@@ -38,7 +38,8 @@ _ERRS = {UDE_E_UNSUPPORTED: "unsupported model configuration", UDE_E_INVALID: "i
 EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_weights_bayes",
                     "ude_rk4_forward", "ude_rk4_backward", "ude_rk4_backward_sir", "ude_dopri5_workspace",
                     "ude_dopri5_forward", "ude_loss_head_workspace", "ude_loss_head_forward",
-                    "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_build_info")
+                    "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_rhs_workspace",
+                    "ude_rhs_forward", "ude_rhs_vjp", "ude_build_info")
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -128,6 +129,12 @@ class NativeLib:
         L.ude_loss_head_backward.restype = i32
         L.ude_loss_head_backward_sir.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_loss_head_backward_sir.restype = i32
+        L.ude_rhs_workspace.argtypes = [pdesc, pprob, i32, ctypes.POINTER(ctypes.c_int64)]
+        L.ude_rhs_workspace.restype = i32
+        L.ude_rhs_forward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp]
+        L.ude_rhs_forward.restype = i32
+        L.ude_rhs_vjp.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_rhs_vjp.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -204,6 +211,20 @@ class NativeLib:
     def loss_backward_sir(self, desc, T, S, B, latent, W, b, y, grad, ws, dlat_sir, dW, db, stream) -> None:
         check(self.lib.ude_loss_head_backward_sir(ctypes.byref(desc), int(T), int(S), int(B), latent, W, b, y, grad,
                                                   ws, dlat_sir, dW, db, stream), "ude_loss_head_backward_sir")
+
+    def rhs_workspace(self, desc, prob, device: int) -> int:
+        out = ctypes.c_int64(0)
+        check(self.lib.ude_rhs_workspace(ctypes.byref(desc), ctypes.byref(prob), int(device), ctypes.byref(out)),
+              "ude_rhs_workspace")
+        return int(out.value)
+
+    def rhs_forward(self, desc, prob, pack, x, f, rates, fa, stream) -> None:
+        check(self.lib.ude_rhs_forward(ctypes.byref(desc), ctypes.byref(prob), pack, x, f, rates, fa, stream),
+              "ude_rhs_forward")
+
+    def rhs_vjp(self, desc, prob, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, stream) -> None:
+        check(self.lib.ude_rhs_vjp(ctypes.byref(desc), ctypes.byref(prob), pack, x, cot_f, cot_rates, cot_fa, dx,
+                                   ws, dparams, stream), "ude_rhs_vjp")
 
     def build_info(self) -> str:
         return self.lib.ude_build_info().decode()

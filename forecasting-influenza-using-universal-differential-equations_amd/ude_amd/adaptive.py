@@ -79,7 +79,7 @@ def fused_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
 # ---------------------------------------------------------------------------
 # eager (any callable, differentiable)
 # ---------------------------------------------------------------------------
-def _rms(x: torch.Tensor) -> torch.Tensor:
+def _rms_default(x: torch.Tensor) -> torch.Tensor:
     return x.abs().pow(2).mean().sqrt()
 
 
@@ -88,7 +88,10 @@ def _dot(ks: List[torch.Tensor], c: torch.Tensor) -> torch.Tensor:
 
 
 def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,
-                 max_num_steps: int = MAX_NUM_STEPS) -> torch.Tensor:
+                 max_num_steps: int = MAX_NUM_STEPS, norm=None) -> torch.Tensor:
+    """``norm``: torchdiffeq's error norm (default the RMS over every element, ``_rms_norm``);
+    odeint_adjoint passes its mixed norm over the augmented state's pieces."""
+    _rms = _rms_default if norm is None else norm
     ydt = y0.dtype
     dev = y0.device
     tt = t.to(device=dev, dtype=torch.float64)

@@ -1,0 +1,174 @@
+"""``odeint_adjoint`` with torchdiffeq's signature and semantics (0.2.x ``adjoint.py``).
+
+BASELINE configs[2] ("Dopri5 adaptive stepping + dense output + adjoint backward"); the
+reference imports the solver API (lib/VAE.py:5) but never calls the adjoint, so
+the specification is torchdiffeq's published algorithm:
+
+* forward: ``odeint(func, y0, t, rtol, atol, method, options)`` without autograd -- for a UDE
+  module on a HIP device the fused gfx950 dopri5 solve (csrc/ude_dopri5.h);
+* backward: for i = T-1 .. 1, solve the augmented system
+  ``[vjp_t, y, a_y, a_theta]`` from t[i] back to t[i-1] with the adjoint method (default: the
+  forward method) and tolerances (default: the forward ones), the augmented dynamics
+  ``(vjp_t, f(t, y), -a_y^T df/dy, -a_y^T df/dtheta)`` run backwards in time (torchdiffeq
+  negates t and the function, ``_ReverseFunc``), with the error norm
+  ``max(|vjp_t|, rms(y), rms(a_y), max_p rms(a_theta_p))`` (``default_adjoint_norm``; the
+  'seminorm' option drops the parameter term); after each segment y is reset to the forward
+  solution at t[i-1] and a_y receives the output cotangent there.
+* the forward solve runs under no_grad, so quantities the RHS records on the side (params /
+  tracker, hence posterior() / the Fa norm) carry no gradient, as in torchdiffeq.
+
+Every augmented evaluation calls the RHS module and ``torch.autograd.grad`` through it: for
+the UDE modules on a HIP device that is one gfx950 evaluation kernel + one VJP kernel
+(ude_amd/eval_rhs.py).  The augmented state lives in one flat tensor (torchdiffeq's
+``_TupleFunc`` flattening) stepped by ude_amd.adaptive.eager_dopri5 or the fixed grids.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+
+from . import adaptive as _adaptive
+
+
+def _rms(x: torch.Tensor) -> torch.Tensor:
+    return x.abs().pow(2).mean().sqrt()
+
+
+def _mixed_norm(tensors: Sequence[torch.Tensor]):
+    if len(tensors) == 0:
+        return 0.0
+    return max([_rms(x) for x in tensors])
+
+
+class _Flat:
+    """Shapes of a tuple state and the flatten / split maps (torchdiffeq ``_TupleFunc``)."""
+
+    def __init__(self, shapes: Sequence[torch.Size]):
+        self.shapes = list(shapes)
+        self.sizes = [int(torch.Size(s).numel()) for s in self.shapes]
+
+    def flat(self, tensors: Sequence[torch.Tensor]) -> torch.Tensor:
+        return torch.cat([x.reshape(-1) for x in tensors])
+
+    def split(self, flat: torch.Tensor) -> List[torch.Tensor]:
+        out, off = [], 0
+        for s, n in zip(self.shapes, self.sizes):
+            out.append(flat[off:off + n].view(s))
+            off += n
+        return out
+
+
+def find_parameters(module) -> List[torch.Tensor]:
+    return [p for p in module.parameters() if p.requires_grad]
+
+
+def _solve_segment(aug_func, flat: _Flat, state: List[torch.Tensor], t_from, t_to, rtol, atol, method, options,
+                   norm_of_tuple):
+    """odeint(augmented_dynamics, state, [t_from, t_to]) with t_to < t_from, returning the state
+    at t_to: solved forwards in s = -t on the negated function (torchdiffeq _ReverseFunc)."""
+    y0 = flat.flat(state)
+    s_pair = torch.stack([-t_from, -t_to])
+
+    def f_rev(s, yf):
+        return -flat.flat(aug_func(-s, flat.split(yf)))
+
+    opts = dict(options or {})
+    if method == "dopri5":
+        norm = lambda v: norm_of_tuple(flat.split(v))
+        sol = _adaptive.eager_dopri5(f_rev, y0, s_pair, rtol, atol, opts.pop("first_step", None),
+                                     opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS), norm=norm)
+    elif method in ("rk4", "euler", "midpoint"):
+        from .solvers import eager_fixed_grid
+        sol = eager_fixed_grid(f_rev, y0, s_pair, method, opts.pop("step_size", None))
+    else:
+        raise NotImplementedError(f"adjoint_method '{method}' is not implemented (dopri5 / rk4 / euler / midpoint are)")
+    return flat.split(sol[1])
+
+
+class _OdeintAdjoint(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, func, y0, t, rtol, atol, method, options, adjoint_rtol, adjoint_atol, adjoint_method,
+                adjoint_options, t_requires_grad, *adjoint_params):
+        from .solvers import odeint
+        with torch.no_grad():
+            ans = odeint(func, y0, t, rtol=rtol, atol=atol, method=method, options=options)
+        ctx.func = func
+        ctx.cfg = (adjoint_rtol, adjoint_atol, adjoint_method, adjoint_options, t_requires_grad)
+        ctx.save_for_backward(t, ans, *adjoint_params)
+        return ans
+
+    @staticmethod
+    def backward(ctx, grad_y):
+        func = ctx.func
+        adjoint_rtol, adjoint_atol, adjoint_method, adjoint_options, t_requires_grad = ctx.cfg
+        t, y, *adjoint_params = ctx.saved_tensors
+        adjoint_params = tuple(adjoint_params)
+        options = dict(adjoint_options or {})
+        seminorm = options.pop("norm", None) == "seminorm"
+
+        def adjoint_norm(parts):
+            vt, yy, ay, *ap = parts
+            n = torch.max(torch.stack([vt.abs().reshape(()), _rms(yy), _rms(ay)]))
+            if not seminorm and ap:
+                n = torch.max(n, _mixed_norm(ap))
+            return n
+
+        def augmented_dynamics(tt, y_aug):
+            yy, adj_y = y_aug[1], y_aug[2]
+            with torch.enable_grad():
+                t_ = tt.detach().requires_grad_(True)
+                yv = yy.detach().requires_grad_(True)
+                # no gradient wrt time unless t requires it (torchdiffeq: func(t if t_requires_grad else t_, y))
+                func_eval = func(t_ if t_requires_grad else tt.detach(), yv)
+                grads = torch.autograd.grad(func_eval, (t_, yv) + adjoint_params, -adj_y, allow_unused=True)
+            vjp_t, vjp_y, *vjp_params = grads
+            vjp_t = torch.zeros_like(tt) if vjp_t is None else vjp_t
+            vjp_y = torch.zeros_like(yy) if vjp_y is None else vjp_y
+            vjp_params = [torch.zeros_like(p) if g is None else g for p, g in zip(adjoint_params, vjp_params)]
+            return [vjp_t.reshape(()).to(yy.dtype), func_eval.detach(), vjp_y.detach()] + \
+                [g.detach() for g in vjp_params]
+
+        with torch.no_grad():
+            zero = torch.zeros((), dtype=y.dtype, device=y.device)
+            aug_state = [zero, y[-1], grad_y[-1]] + [torch.zeros_like(p) for p in adjoint_params]
+            flat = _Flat([a.shape for a in aug_state])
+            time_vjps = torch.empty(len(t), dtype=t.dtype, device=t.device) if t_requires_grad else None
+            for i in range(len(t) - 1, 0, -1):
+                if t_requires_grad:
+                    fe = func(t[i], y[i])
+                    dLd_cur_t = fe.reshape(-1).dot(grad_y[i].reshape(-1))
+                    aug_state[0] = aug_state[0] - dLd_cur_t
+                    time_vjps[i] = dLd_cur_t
+                aug_state = list(_solve_segment(augmented_dynamics, flat, aug_state, t[i], t[i - 1], adjoint_rtol,
+                                                adjoint_atol, adjoint_method, options, adjoint_norm))
+                aug_state[1] = y[i - 1]
+                aug_state[2] = aug_state[2] + grad_y[i - 1]
+            if t_requires_grad:
+                time_vjps[0] = -aug_state[0]
+        adj_y = aug_state[2]
+        adj_params = aug_state[3:]
+        return (None, adj_y, time_vjps, None, None, None, None, None, None, None, None, None, *adj_params)
+
+
+def odeint_adjoint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None,
+                   adjoint_rtol=None, adjoint_atol=None, adjoint_method=None, adjoint_options=None,
+                   adjoint_params=None):
+    """torchdiffeq.odeint_adjoint (tensor y0; no events)."""
+    if event_fn is not None:
+        raise NotImplementedError("event handling is not supported")
+    if not isinstance(func, torch.nn.Module) and adjoint_params is None:
+        raise ValueError("func must be an instance of nn.Module to specify the adjoint parameters; "
+                         "alternatively they can be specified explicitly via the `adjoint_params` argument.")
+    method = "dopri5" if method is None else method
+    adjoint_params = tuple(find_parameters(func)) if adjoint_params is None else tuple(adjoint_params)
+    adjoint_params = tuple(p for p in adjoint_params if p.requires_grad)
+    adjoint_rtol = rtol if adjoint_rtol is None else adjoint_rtol
+    adjoint_atol = atol if adjoint_atol is None else adjoint_atol
+    if adjoint_method is None:
+        adjoint_method = method
+    if adjoint_options is None:
+        adjoint_options = {k: v for k, v in (options or {}).items() if k != "norm"} \
+            if adjoint_method == method else {}
+    return _OdeintAdjoint.apply(func, y0, t, rtol, atol, method, options, adjoint_rtol, adjoint_atol,
+                                adjoint_method, adjoint_options, bool(t.requires_grad), *adjoint_params)

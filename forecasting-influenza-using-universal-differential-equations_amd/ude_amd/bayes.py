@@ -121,9 +121,35 @@ class _BayesBase(_UDEModule):
             sds += [lay.w_std, lay.b_std]
         return mus, sds
 
+    def _eval_weights(self) -> List[torch.Tensor]:
+        """This evaluation's weight sample, drawn and formed by the layers exactly as their
+        forward does (make_z per layer in call order; w = mean + z * |std|, :43-48) -- or, with
+        a stream set by ``set_eps_stream``, its next row (torch parameter order per layer)."""
+        eps = getattr(self, "_eps_next", None)
+        row = None
+        if eps is not None:
+            k = getattr(self, "_eps_row", 0)
+            row = eps[k]
+            self._eps_row = k + 1
+            if self._eps_row >= eps.shape[0]:
+                self._eps_next, self._eps_row = None, 0
+        out: List[torch.Tensor] = []
+        off = 0
+        for lay in self._variational():
+            if row is None:
+                lay.make_z()
+            else:
+                nw, nb = lay.w_mean.numel(), lay.b_mean.numel()
+                lay.z = [row[off:off + nw].view_as(lay.w_mean), row[off + nw:off + nw + nb].view_as(lay.b_mean)]
+                off += nw + nb
+            out += [lay.w_mean + lay.z[0] * torch.abs(lay.w_std), lay.b_mean + lay.z[1] * torch.abs(lay.b_std)]
+        return out
+
     def set_eps_stream(self, eps: Optional[torch.Tensor]) -> None:
-        """Use ``eps`` ((4 * n_steps, n_params)) as the draws of the next fused solve."""
+        """Use ``eps`` ((4 * n_steps, n_params)) as the draws of the next solve: the fused
+        whole-solve kernel takes all of it, evaluations one at a time take a row each."""
         self._eps_next = eps
+        self._eps_row = 0
 
     def take_eps(self, n_eval: int, n_params: int, device) -> torch.Tensor:
         eps = getattr(self, "_eps_next", None)
@@ -145,6 +171,9 @@ class Bayes_Fp(_BayesBase):
         self._init_tracking()
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
         self.params.append(rates)
         return _finish(_sir_flux(rates, x), x)
@@ -163,6 +192,9 @@ class Bayes_Fa(_BayesBase):
         self._init_tracking()
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
         res = _finish(fa, x)
         self.tracker.append(fa)
@@ -185,6 +217,9 @@ class Bayes_FaFp(_BayesBase):
         self._init_tracking()
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
         self.params.append(rates)
         fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)

@@ -41,6 +41,9 @@ PREBUILT += [
     _c("Fa", 1, 8, None, [32, 32]),
     _c("Fp", 1, 6, [24], None),                      # golden: fp_r1_onehidden
     _c("FaFp", 3, 5, [40, 24], [36], ),              # golden: fafp_r3_l5_ragged
+    # golden single-evaluation fixtures rhs_{fp,fa,fafp}_r{1,4} (net [16, 16, 8], aug [16, 12])
+    _c("Fp", 1, 8, [16, 16, 8], None), _c("Fa", 1, 8, None, [16, 12]), _c("FaFp", 1, 8, [16, 16, 8], [16, 12]),
+    _c("Fp", 4, 8, [16, 16, 8], None), _c("Fa", 4, 8, None, [16, 12]), _c("FaFp", 4, 8, [16, 16, 8], [16, 12]),
     # Bayesian RHS (run_ode.py:99 'CONNb' / 'UONNb' / 'SONNb'), US model sizes
     _c("BFaFp", 1, 8, [64, 64, 32], [64, 64]),
     _c("BFp", 1, 8, [64, 64, 32], None),

@@ -143,6 +143,10 @@ class FusedRK4(torch.autograd.Function):
             dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         if dlatent is not None:
             dlatent = dlatent.contiguous().to(torch.float32)
+            if dl3 is not None:                     # other consumers too: one full cotangent
+                dlatent = dlatent.clone()
+                dlatent[..., :3] += dl3
+                dl3 = None
         dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
         dy0 = torch.empty_like(y0)
         slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)

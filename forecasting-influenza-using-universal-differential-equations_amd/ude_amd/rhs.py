@@ -90,6 +90,8 @@ class _UDEModule(nn.Module):
 
     ode_type = "FaFp"
     uncertainty = "none"
+    # forward(t, x) on a HIP device: one gfx950 kernel per evaluation (ude_amd/eval_rhs.py)
+    fused_eval = True
     # opt-in: after a fused solve, fill ``params`` / ``tracker`` with one (N, R, 2) rate tensor /
     # one (N, R, 3) A-net tensor per RHS evaluation, as the reference's forward appends them
     # (lib/models.py:137, :187, :238, :252); recomputed from the solve's stage checkpoints
@@ -187,6 +189,27 @@ class _UDEModule(nn.Module):
     def fa_weight(self) -> float:
         return float(getattr(self, "Fa_w", 1.0))
 
+    def _eval_weights(self) -> List[torch.Tensor]:
+        out: List[torch.Tensor] = []
+        for lin in self.ude_linears():
+            out += [lin.weight, lin.bias]
+        return out
+
+    def _fused_forward(self, x: torch.Tensor):
+        """forward() on the gfx950 evaluation kernel when x lives on a HIP device (else None):
+        the same return value and the same params / tracker entries as the eager code."""
+        if not (x.is_cuda and self.fused_eval):
+            return None
+        from . import eval_rhs
+        if not eval_rhs.eligible(self, x):
+            return None
+        f, rates, fa = eval_rhs.rhs_eval(self, x, self._eval_weights())
+        if rates is not None:
+            self.params.append(rates)
+        if fa is not None:
+            self.tracker.append(fa)
+        return f
+
 
 class Fp(_UDEModule):
     """Physics RHS with MLP-learned SIR rates ("CONN"), lib/models.py:109-156."""
@@ -205,6 +228,9 @@ class Fp(_UDEModule):
         return self.Fp_net
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
         self.params.append(rates)
         return _finish(_sir_flux(rates, x), x)
@@ -229,6 +255,9 @@ class Fa(_UDEModule):
         return self.aug_net
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         fa = _run_stack(self.aug_net, self.flatten(x)).reshape(-1, self.n_regions, 3)
         res = _finish(fa, x)
         self.tracker.append(fa)
@@ -258,6 +287,9 @@ class FaFp(_UDEModule):
         return self.aug_net
 
     def forward(self, t, x):
+        f = self._fused_forward(x)
+        if f is not None:
+            return f
         rates = torch.abs(_run_stack(self.net, x)).reshape(-1, self.n_regions, 2)
         self.params.append(rates)
         fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)

@@ -11,13 +11,16 @@ Dispatch:
   kernels hold) + fp32 state on a HIP device  ->  the fused gfx950 kernel
   (forward + VJP), no fallback: a missing or unloadable library raises;
 * anything else (other callables, CPU tensors, fixed-grid 'euler' /
-  'midpoint' / 'rk4')  ->  the generic step-by-step solver below, which calls
-  ``func`` once per stage exactly as torchdiffeq does.  Setting
-  ``UDE_STRICT=1`` makes a UDE module that would take this path raise instead.
+  'midpoint' / 'rk4', Bayesian models too large for the whole-solve kernel)  ->  the
+  generic step-by-step solver below, which calls ``func`` once per stage exactly as
+  torchdiffeq does; a UDE module on a HIP device then evaluates on the gfx950
+  evaluation + VJP kernels (ude_amd/eval_rhs.py).  ``UDE_STRICT=1`` makes a UDE module
+  whose evaluations would run as PyTorch operators raise instead.
 ``method='dopri5'`` (torchdiffeq's default): the fused gfx950 adaptive solve for
 a UDE module without autograd (ude_amd/adaptive.py, csrc/ude_dopri5.h), else the
-eager differentiable restatement.  Other adaptive methods raise
-NotImplementedError.
+differentiable step-by-step restatement (its evaluations on the gfx950 evaluation
+kernels for a UDE module on a HIP device).  ``odeint_adjoint``: ude_amd/adjoint.py.
+Other adaptive methods raise NotImplementedError.
 """
 from __future__ import annotations
 
@@ -53,6 +56,17 @@ def _check_t(t: torch.Tensor) -> None:
 
 def _needs_grad(func, y0: torch.Tensor) -> bool:
     return torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in func.parameters()))
+
+
+def _strict() -> bool:
+    return os.environ.get("UDE_STRICT", "0") == "1"
+
+
+def _eval_fused(func, y0: torch.Tensor) -> bool:
+    """Whether each evaluation of a step-by-step solve runs on the gfx950 evaluation kernels
+    (ude_amd/eval_rhs.py) -- the module's forward on a HIP device."""
+    from . import eval_rhs
+    return bool(getattr(func, "fused_eval", False)) and eval_rhs.eligible(func, y0)
 
 
 def fusable(func, y0: torch.Tensor) -> bool:
@@ -199,15 +213,15 @@ def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, even
         max_num_steps = options.pop("max_num_steps", _adaptive.MAX_NUM_STEPS)
         if fusable(func, y0) and func.uncertainty == "none" and not _needs_grad(func, y0):
             return _adaptive.fused_dopri5(func, y0, t, rtol, atol, first_step, max_num_steps)
-        if isinstance(func, _UDEModule) and os.environ.get("UDE_STRICT", "0") == "1":
-            raise RuntimeError("UDE_STRICT=1: this dopri5 solve would not run on the fused gfx950 kernel "
+        if isinstance(func, _UDEModule) and _strict() and not _eval_fused(func, y0):
+            raise RuntimeError("UDE_STRICT=1: this dopri5 solve would not run on the fused gfx950 kernels "
                                f"(grad={_needs_grad(func, y0)}, device={y0.device}, dtype={y0.dtype})")
         return _adaptive.eager_dopri5(func, y0, t, rtol, atol, first_step, max_num_steps)
     if method in ADAPTIVE_METHODS:
         raise NotImplementedError(f"method '{method}' is not implemented (rk4 / euler / midpoint / dopri5 are)")
     if method == "rk4" and fusable(func, y0):
         return fused_odeint(func, y0, t, step_size)
-    if isinstance(func, _UDEModule) and os.environ.get("UDE_STRICT", "0") == "1":
-        raise RuntimeError("UDE_STRICT=1: this solve would not run on the fused gfx950 kernel "
+    if isinstance(func, _UDEModule) and _strict() and not _eval_fused(func, y0):
+        raise RuntimeError("UDE_STRICT=1: this solve would not run on the fused gfx950 kernels "
                            f"(method={method}, device={y0.device}, dtype={y0.dtype})")
     return eager_fixed_grid(func, y0, t, method, step_size)

@@ -135,10 +135,11 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
 
 /* Backward with the S, I, R output cotangents handed over compactly: the
  * training loss terms read only latent[..., :3] (lib/VAE.py:138, :189 -- Decoder and
- * latent_init_loss), so their cotangent has zeros in every dim >= 3.  dlatent_sir: (T, N, R, 3)
- * (nullable), added to dlatent (T, N, R, L) (nullable: all zero); with the fused loss head
- * (ude_loss_head_backward_sir) neither the zero dims nor a full-size cotangent are written or
- * read.  Replaces the same autograd backward as ude_rk4_backward (lib/VAE.py:203). */
+ * latent_init_loss), so their cotangent has zeros in every dim >= 3.  Exactly one of dlatent
+ * (T, N, R, L) and dlatent_sir (T, N, R, 3) is given (the other NULL); with dlatent_sir the
+ * dims >= 3 are zero.  With the fused loss head (ude_loss_head_backward_sir) neither the zero
+ * dims nor a full-size cotangent are written or read.  Replaces the same autograd backward as
+ * ude_rk4_backward (lib/VAE.py:203). */
 int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
                          const void* sched, const float* y0, const float* ckpt,
                          const float* dlatent, const float* dlatent_sir, const float* stats_out,
@@ -199,6 +200,27 @@ int ude_loss_head_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t 
 int ude_loss_head_backward_sir(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* latent,
                                const float* W, const float* b, const float* y, const float* grad, void* ws,
                                float* dlatent_sir, float* dW, float* db, ude_stream_t stream);
+
+/* ---- one evaluation of the right-hand side and its VJP ---------------------------------
+ * Fp / Fa / FaFp.forward(t, x) (lib/models.py:129-146, :177-188, :230-254) for every trajectory
+ * of a batch: f (N, R, L) = the returned derivative (dims >= 3 zero, masked outside [-1, 2]),
+ * rates (N, R, 2) = |net(x)| (what params.append records, :137 / :238; nullable) and
+ * fa (N, R, 3) = aug_net(x) (tracker.append, :187 / :252; nullable).  ude_rhs_vjp: given the
+ * cotangents of f (dims >= 3 ignored), rates and fa (both nullable: zero) writes dx (N, R, L)
+ * and dparams (torch parameter order, ude_query's n_params) -- what autograd computes through
+ * one forward() call.  These serve the solves that are not the fused RK4 kernel (adaptive
+ * solves with autograd, odeint_adjoint, euler / midpoint) and, with each evaluation's sampled
+ * weights packed by ude_pack_weights as a deterministic model, the Bayesian RHS
+ * (models_bayes.py:43-48).  Deterministic kinds only; p->n_traj = N, p->fa_w = FaFp.Fa_w;
+ * ws: ude_rhs_workspace() bytes. */
+int ude_rhs_workspace(const UdeModelDesc* m, const UdeProblem* p, int device, int64_t* ws_bytes);
+
+int ude_rhs_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x, float* f,
+                    float* rates, float* fa, ude_stream_t stream);
+
+int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x, const float* cot_f,
+                const float* cot_rates, const float* cot_fa, float* dx, void* ws, float* dparams,
+                ude_stream_t stream);
 
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);

@@ -82,12 +82,12 @@ def _lincomb(ks: List[torch.Tensor], coefs: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def select_initial_step(func, t0, y0, f0, rtol, atol):
+def select_initial_step(func, t0, y0, f0, rtol, atol, norm=rms_norm):
     """``_select_initial_step(func, t0, y0, order=4, rtol, atol, norm, f0)``."""
     dt = y0.dtype
     scale = atol + torch.abs(y0) * rtol
-    d0 = rms_norm(y0 / scale).abs()
-    d1 = rms_norm(f0 / scale).abs()
+    d0 = norm(y0 / scale).abs()
+    d1 = norm(f0 / scale).abs()
     if d0 < 1e-5 or d1 < 1e-5:
         h0 = torch.tensor(1e-6, dtype=dt)
     else:
@@ -95,7 +95,7 @@ def select_initial_step(func, t0, y0, f0, rtol, atol):
     h0 = h0.abs()
     y1 = y0 + h0 * f0
     f1 = func(t0 + h0, y1)
-    d2 = torch.abs(rms_norm((f1 - f0) / scale) / h0)
+    d2 = torch.abs(norm((f1 - f0) / scale) / h0)
     if d1 <= 1e-15 and d2 <= 1e-15:
         h1 = torch.max(torch.tensor(1e-6, dtype=dt), h0 * 1e-3)
     else:
@@ -144,8 +144,10 @@ class Dopri5Stats:
 
 
 def odeint_dopri5(func: Callable, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9,
-                  first_step=None, max_num_steps: int = 2 ** 31 - 1, stats: Optional[Dopri5Stats] = None):
-    """``odeint(func, y0, t, rtol, atol, method='dopri5')`` (no events, no step_t / jump_t)."""
+                  first_step=None, max_num_steps: int = 2 ** 31 - 1, stats: Optional[Dopri5Stats] = None,
+                  norm: Callable = rms_norm):
+    """``odeint(func, y0, t, rtol, atol, method='dopri5')`` (no events, no step_t / jump_t);
+    ``norm`` = the solver's error norm (``options['norm']``, default ``_rms_norm``)."""
     st = stats if stats is not None else Dopri5Stats()
     sd = y0.dtype
     tt = t.to(torch.float64)
@@ -165,7 +167,7 @@ def odeint_dopri5(func: Callable, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, 
     f0 = f(t0.to(sd), y0)
     if first_step is None:
         dt = select_initial_step(f, t0.to(sd), y0, f0, rtol_t.to(sd) if sd == torch.float64 else rtol_t,
-                                 atol_t.to(sd) if sd == torch.float64 else atol_t)
+                                 atol_t.to(sd) if sd == torch.float64 else atol_t, norm)
     else:
         dt = torch.tensor(first_step, dtype=torch.float64)
     y = y0
@@ -190,7 +192,7 @@ def odeint_dopri5(func: Callable, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, 
             f1 = ks[-1]
             err = _lincomb(ks, dts * c_err)
             error_tol = atol_t + rtol_t * torch.max(y.abs(), y1.abs())
-            error_ratio = rms_norm(err / error_tol).abs()
+            error_ratio = norm(err / error_tol).abs()
             accept = bool(error_ratio <= 1)
             st.n_steps += 1
             st.steps.append((float(ts), float(dt), float(error_ratio), accept))

@@ -1,0 +1,149 @@
+"""odeint_adjoint (torchdiffeq's adjoint API; BASELINE configs[2] "adjoint backward").
+
+CPU: known-answer tests of the adjoint gradient (linear ODE vs the matrix exponential), the
+product adjoint (ude_amd/adjoint.py) against the oracle's independent restatement
+(oracle/ude_oracle_adjoint.py), and the adjoint against autograd through the forward solve
+at tight tolerances.  GPU: UDE modules on the MI355X -- forward = the fused dopri5 solve,
+backward = the augmented solve whose every evaluation is the gfx950 evaluation + VJP kernels
+-- against the oracle adjoint in fp64 on the host.
+
+torchdiffeq is absent (unpinned dependency of the reference), so parity with torchdiffeq
+itself is unpinned; the KATs pin the algorithm."""
+import pytest
+import torch
+
+from helpers import normwise_rel
+from oracle.ude_oracle import OracleRHS
+from oracle.ude_oracle_adjoint import adjoint_backward
+from oracle.ude_oracle_dopri5 import odeint_dopri5
+
+
+class _Linear(torch.nn.Module):
+    def __init__(self, A):
+        super().__init__()
+        self.A = torch.nn.Parameter(A.clone())
+
+    def forward(self, t, y):
+        return y @ self.A.T
+
+
+def test_adjoint_linear_ode_matches_matrix_exponential(pkg):
+    from torchdiffeq import odeint_adjoint
+    torch.manual_seed(0)
+    A = torch.randn(3, 3, dtype=torch.float64) * 0.5
+    y0 = torch.randn(4, 3, dtype=torch.float64).requires_grad_(True)
+    t = torch.tensor([0.0, 0.4, 1.1], dtype=torch.float64)
+    c = torch.randn(3, 4, 3, dtype=torch.float64)
+    f = _Linear(A)
+    ys = odeint_adjoint(f, y0, t, rtol=1e-10, atol=1e-12, method="dopri5")
+    (ys * c).sum().backward()
+    Ar = A.clone().requires_grad_(True)
+    y0r = y0.detach().clone().requires_grad_(True)
+    yr = torch.stack([y0r @ torch.linalg.matrix_exp(Ar * float(tt)).T for tt in t])
+    (yr * c).sum().backward()
+    assert normwise_rel(ys.detach(), yr.detach()) < 1e-8
+    assert normwise_rel(y0.grad, y0r.grad) < 1e-7
+    assert normwise_rel(f.A.grad, Ar.grad) < 1e-7
+
+
+def _uoracle(pkg, kind, R, dtype):
+    torch.manual_seed(2)
+    if kind == "FaFp":
+        m = pkg.FaFp(R, latent_dim=8, net_sizes=[16, 16, 8], aug_net_sizes=[16, 12])
+        m.Fa_w = 0.6
+    elif kind == "Fp":
+        m = pkg.Fp(R, latent_dim=8, net_sizes=[16, 16, 8])
+    else:
+        m = pkg.Fa(R, latent_dim=8, aug_net_sizes=[16, 12])
+    return m.to(dtype)
+
+
+def _y0(N, R, dtype, seed=4):
+    g = torch.Generator().manual_seed(seed)
+    S = torch.rand(N, R, generator=g) * 0.4 + 0.5
+    I = torch.rand(N, R, generator=g) * 0.05
+    return torch.cat([S[..., None], I[..., None], (1 - S - I)[..., None], torch.randn(N, R, 5, generator=g)],
+                     -1).to(dtype)
+
+
+@pytest.mark.parametrize("kind", ["FaFp", "Fp", "Fa"])
+def test_adjoint_matches_oracle_restatement_cpu(pkg, kind):
+    """Product adjoint (eager RHS on the host) vs the oracle's restatement, fp64."""
+    from torchdiffeq import odeint_adjoint
+    mod = _uoracle(pkg, kind, 1, torch.float64)
+    y0 = _y0(6, 1, torch.float64).requires_grad_(True)
+    t = torch.tensor([0.0, 0.5, 1.0, 2.0], dtype=torch.float64)
+    c = torch.randn((4,) + tuple(y0.shape), generator=torch.Generator().manual_seed(9), dtype=torch.float64)
+    ys = odeint_adjoint(mod, y0, t, rtol=1e-8, atol=1e-10)
+    (ys * c).sum().backward()
+    rhs = OracleRHS.from_module(mod, torch.float64).requires_grad_()
+    with torch.no_grad():
+        yr = odeint_dopri5(rhs, y0.detach(), t, rtol=1e-8, atol=1e-10)
+    dy0, dps = adjoint_backward(rhs, rhs.weights(), t, yr, c, 1e-8, 1e-10)
+    # same algorithm, different fp64 operation orders (matmul vs sum of products in the
+    # stage combinations): step sizes agree to rounding
+    assert normwise_rel(ys.detach(), yr) < 1e-10
+    assert normwise_rel(y0.grad, dy0) < 1e-7
+    grads = [p.grad for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
+    for a, b in zip(grads, dps):
+        assert normwise_rel(a, b) < 1e-7
+
+
+def test_adjoint_converges_to_true_gradient(pkg):
+    """Adjoint gradients approach the exact gradient (backprop through a fine fixed-step RK4,
+    O(h^4)) as the tolerances shrink.  (Backprop through the adaptive solve itself is not the
+    reference: it also differentiates the step-size controller.)"""
+    from torchdiffeq import odeint, odeint_adjoint
+    mod = _uoracle(pkg, "FaFp", 1, torch.float64)
+    y0 = _y0(5, 1, torch.float64)
+    t = torch.tensor([0.0, 1.0, 2.5], dtype=torch.float64)
+    c = torch.randn((3,) + tuple(y0.shape), generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    gt = y0.clone().requires_grad_(True)
+    (odeint(mod, gt, t, method="rk4", options=dict(step_size=2.5e-3)) * c).sum().backward()
+    errs = []
+    for tol in (1e-5, 1e-9):
+        ga = y0.clone().requires_grad_(True)
+        (odeint_adjoint(mod, ga, t, rtol=tol, atol=tol * 1e-2) * c).sum().backward()
+        errs.append(normwise_rel(ga.grad, gt.grad))
+    assert errs[1] < 1e-7 and errs[1] < 1e-2 * errs[0], errs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,R", [("FaFp", 1), ("Fp", 1), ("Fa", 1), ("FaFp", 49)])
+def test_fused_adjoint_matches_oracle(pkg, kind, R):
+    from torchdiffeq import odeint_adjoint
+    if R == 49:
+        torch.manual_seed(2)
+        mod = pkg.FaFp(49, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+    else:
+        mod = _uoracle(pkg, kind, R, torch.float32)
+        if kind == "Fp":
+            mod = pkg.Fp(1, latent_dim=8, net_sizes=[32, 32])
+        elif kind == "Fa":
+            mod = pkg.Fa(1, latent_dim=8, aug_net_sizes=[64, 64])
+        else:
+            mod = pkg.FaFp(1, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+    N = 24 if R == 49 else 40
+    y0 = _y0(N, R, torch.float32)
+    t = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float32)
+    c = torch.randn((3,) + tuple(y0.shape), generator=torch.Generator().manual_seed(3))
+    rtol, atol = 1e-6, 1e-8
+    rhs = OracleRHS.from_module(mod, torch.float64).requires_grad_()
+    with torch.no_grad():
+        yr = odeint_dopri5(rhs, y0.double(), t, rtol=rtol, atol=atol)
+    dy0, dps = adjoint_backward(rhs, rhs.weights(), t, yr, c.double(), rtol, atol)
+    # the same adjoint restated in fp32: the bar is max(1e-4, 2 x its distance to fp64)
+    r32 = OracleRHS.from_module(mod, torch.float32).requires_grad_()
+    with torch.no_grad():
+        y32 = odeint_dopri5(r32, y0, t, rtol=rtol, atol=atol)
+    d32, p32 = adjoint_backward(r32, r32.weights(), t, y32, c, rtol, atol)
+    bar = lambda a, b: max(1e-4, 2.0 * normwise_rel(a, b))
+    mg = mod.to("cuda")
+    yg = y0.to("cuda").requires_grad_(True)
+    ys = odeint_adjoint(mg, yg, t.to("cuda"), rtol=rtol, atol=atol)
+    (ys * c.to("cuda")).sum().backward()
+    assert normwise_rel(ys.detach(), yr) < 1e-5
+    assert normwise_rel(yg.grad, dy0) < bar(d32, dy0), normwise_rel(yg.grad, dy0)
+    grads = [p.grad for lin in mg.ude_linears() for p in (lin.weight, lin.bias)]
+    for i, (a, b) in enumerate(zip(grads, dps)):
+        assert normwise_rel(a, b) < bar(p32[i], b), (i, normwise_rel(a, b), bar(p32[i], b))

@@ -69,7 +69,7 @@ def test_loss_head_rejects_oversized_sample_tile(pkg):
     assert not loss_head.eligible(ode, lat[..., 1:], lin, S, B)              # not the model's L
 
 
-def _vae_step(S, fused_ok, monkeypatch):
+def _vae_step(S, fused_ok, monkeypatch, mse=False):
     import lib.VAE as vae_mod
     import lib.models as models
     from ude_amd import loss_head
@@ -90,7 +90,7 @@ def _vae_step(S, fused_ok, monkeypatch):
     monkeypatch.setattr(torch, "randn", lambda *a, **k: eps.clone())
     y_pred = model(x, t, n_samples=S, training=True)
     monkeypatch.setattr(torch, "randn", real_randn)
-    losses = {"nll": True, "mse": False, "kl_z": True, "kl_p": True, "Fa_norm": 0.1, "reg_loss": True,
+    losses = {"nll": True, "mse": mse, "kl_z": True, "kl_p": True, "Fa_norm": 0.1, "reg_loss": True,
               "anneal": True}
     took_fused = model._fused_head(y_pred, y, losses) is not None
     loss, data, names = model.calc_loss(y_pred, y, losses)
@@ -139,5 +139,18 @@ def test_compact_sir_cotangent_matches_full(pkg, monkeypatch):
     f2, loss_f, g_f = _vae_step(64, True, monkeypatch)
     assert f1 and f2 and not calls
     assert torch.equal(loss_c, loss_f)
+    for k in g_f:
+        assert torch.equal(g_c[k], g_f[k]), (k, normwise_rel(g_c[k], g_f[k]))
+
+
+@pytest.mark.gpu
+def test_compact_sir_cotangent_with_other_consumers(pkg, monkeypatch):
+    """The latent also feeds the mse term (through the decoder): the solve's backward gets the
+    full cotangent of that path plus the loss head's compact deposit, merged once."""
+    from ude_amd import loss_head
+    f1, loss_c, g_c = _vae_step(64, True, monkeypatch, mse=True)
+    monkeypatch.setattr(loss_head, "COMPACT", False)
+    f2, loss_f, g_f = _vae_step(64, True, monkeypatch, mse=True)
+    assert f1 and f2 and torch.equal(loss_c, loss_f)
     for k in g_f:
         assert torch.equal(g_c[k], g_f[k]), (k, normwise_rel(g_c[k], g_f[k]))

@@ -274,6 +274,93 @@ def loss_head_line(pkg, w, dev, reps=20):
                          "algorithmic_bytes": {"fwd": lat_bytes, "bwd": 2 * lat_bytes}}}
 
 
+def adjoint_line(pkg, w, dev, T=2, rtol=1e-5, atol=1e-7, seminorm=True):
+    """BASELINE configs[2] forward + adjoint backward on the state49 batch: odeint_adjoint
+    (torchdiffeq semantics) -- forward = the fused dopri5 solve, backward = the augmented
+    dopri5 solve whose every evaluation is the gfx950 evaluation + VJP kernels."""
+    from torchdiffeq import odeint_adjoint
+    mod, y0, t, _ = build(pkg, w, dev, seed=78)
+    td = t[:T].to(dev)
+    dl = torch.randn((T,) + tuple(y0.shape), device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+    y0 = y0.detach().requires_grad_(True)
+
+    def step():
+        mod.clear_tracking()
+        mod.zero_grad(set_to_none=True)
+        y0.grad = None
+        lat = odeint_adjoint(mod, y0, td, rtol=rtol, atol=atol,
+                             adjoint_options=dict(norm="seminorm") if seminorm else None)
+        info = dict(mod.last_solve_info)
+        (lat * dl).sum().backward()
+        info.update(mod.last_adjoint_info)
+        return info
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    info = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": f"state49 batch ({w['n_traj']} trajectories, R=49), t = {T - 1} weekly interval(s), "
+                        f"odeint_adjoint dopri5 rtol {rtol:g} atol {atol:g}"
+                        f"{' adjoint_options norm=seminorm' if seminorm else ''}, forward + adjoint backward",
+            "ms_per_step": el * 1e3, "forward_steps": info["n_steps"], "forward_evals": info["n_evals"],
+            "adjoint_evals": info["augmented_evals"],
+            "ms_per_adjoint_eval": el * 1e3 / max(info["augmented_evals"], 1),
+            "rhs_evals_per_s_incl_vjp": (info["n_evals"] + info["augmented_evals"]) * w["n_traj"] / el}
+
+
+def bayes_large_line(pkg, dev, steps=3):
+    """SURVEY 8f row 1 at the state model's size: Bayes_FaFp R=49 (run_ode.py 'UONNb'), 20,480
+    trajectories x 8 weekly RK4 steps, fwd+bwd; each RHS evaluation draws its weight sample and
+    runs on the gfx950 evaluation + VJP kernels (the whole-solve kernel's two register dW sets
+    do not fit this size)."""
+    w = dict(WORKLOADS["state49"], kind="Bayes_FaFp")
+    mod, y0, t, dlat = build(pkg, w, dev, seed=21)
+    el, k = time_steps(pkg, None, mod, y0, t, dlat, 1, steps, 1, lambda: None, dev)
+    v = w["n_traj"] * (len(t) - 1) * steps / el
+    return {"workload": "Bayes_FaFp R=49, 20480 trajectories x 8 weekly RK4 steps (per-evaluation kernels)",
+            "traj_steps_per_s": v, "ms_per_step": el / steps * 1e3}
+
+
+def train_head_line(pkg, w, dev, reps=10):
+    """one training step of the state49 workload through the fused solve and
+    the fused loss head (decoder + nll_loss + latent_init_loss), backward into the solve: with
+    the S, I, R-only cotangent hand-off (no full-size d latent written or read) vs without."""
+    import lib.models as models
+    from ude_amd import loss_head
+    mod, y0, t, _ = build(pkg, w, dev, seed=31)
+    S, B, R = 64, w["n_traj"] // 64, w["R"]
+    dec = models.Decoder(R, w["L"], 1).to(dev)
+    y = torch.rand(B, len(t), R, device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+    lin = dec.decoder[-1]
+
+    def step():
+        mod.clear_tracking()
+        mod.zero_grad(set_to_none=True)
+        y0.grad = None
+        lat = pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+        nll, reg = loss_head.fused_loss_head(mod, lat, lin, y, S, B)
+        post = mod.posterior()
+        loss = nll + 0.1 * reg + post.loc.sum() + post.scale.sum() + 0.1 * torch.norm(torch.stack(mod.tracker))
+        loss.backward()
+
+    out = {}
+    for compact in (True, False):
+        loss_head.COMPACT = compact
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        torch.cuda.synchronize()
+        out["ms_per_step_sir_handoff" if compact else "ms_per_step_full_dlatent"] = (time.perf_counter() - t0) / reps * 1e3
+    loss_head.COMPACT = True
+    n = w["n_traj"] * len(t) * R
+    return dict(workload="state49 training step: fused RK4 solve + fused loss head, fwd+bwd", **out,
+                dlatent_bytes_full=n * w["L"] * 4, dlatent_bytes_sir=n * 3 * 4)
+
+
 def _cpu_copy(mod):
     import copy
     mod.clear_tracking()
@@ -442,13 +529,22 @@ def main():
             res["strong_scaling"] = strong
     extra = rank == 0 and world == 1 and not args.no_extra and args.workload == "state49" and not args.rehearse_cpu
     if extra:
-        res["north_star_M1"] = dict(extra_line(pkg, udist, "us_northstar", dev, barrier), target_rhs_evals_per_s=1e7)
-        res["north_star_M1_fp32"] = extra_line(pkg, udist, "us_fp32", dev, barrier)
-        res["M2_state49_n2048"] = extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=10)
-        res["M3_states_r1"] = extra_line(pkg, udist, "m3_states_r1", dev, barrier)
-        res["bayes_M1"] = extra_line(pkg, udist, "bayes_us", dev, barrier)
-        res["dopri5_state49"] = dopri5_line(pkg, w, dev)
-        res["loss_head_state49"] = loss_head_line(pkg, w, dev)
+        lines = [("north_star_M1", lambda: dict(extra_line(pkg, udist, "us_northstar", dev, barrier),
+                                                target_rhs_evals_per_s=1e7)),
+                 ("north_star_M1_fp32", lambda: extra_line(pkg, udist, "us_fp32", dev, barrier)),
+                 ("M2_state49_n2048", lambda: extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=10)),
+                 ("M3_states_r1", lambda: extra_line(pkg, udist, "m3_states_r1", dev, barrier)),
+                 ("bayes_M1", lambda: extra_line(pkg, udist, "bayes_us", dev, barrier)),
+                 ("dopri5_state49", lambda: dopri5_line(pkg, w, dev)),
+                 ("dopri5_adjoint_state49", lambda: adjoint_line(pkg, w, dev)),
+                 ("bayes_state49", lambda: bayes_large_line(pkg, dev)),
+                 ("loss_head_state49", lambda: loss_head_line(pkg, w, dev)),
+                 ("train_step_head_state49", lambda: train_head_line(pkg, w, dev))]
+        for name, fn in lines:
+            t0 = time.perf_counter()
+            res[name] = fn()
+            torch.cuda.empty_cache()
+            print(f"[bench] {name}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.rehearse_cpu:
         res["cpu_baseline"] = cpu_baseline(w, mod, threads=CPU_THREADS)
         res["cpu_baseline_1thread"] = cpu_baseline(w, mod, threads=1)

@@ -195,7 +195,7 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
   f4 dw[NDWn], dws[1], g0t[NZn], c1[NZn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
-  WRegs<M, W, true> wr;
+  WRegs<M, W, true, true> wr;                      // recomputes the forward: all fragments
   wr.load(rs, lane);
   #pragma unroll 1
   for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;

@@ -232,17 +232,19 @@ struct NoWRegs {
   static constexpr bool ON = false;
   f4 wf[1], wb[1], wx[1];
 };
-template <class M, int W, bool BWD>
+template <class M, int W, bool BWD, bool NEED_F_ = !BWD || !M::STORE_ACT>
 struct WRegs {
   static constexpr bool ON = M::WREG;
-  static constexpr int NF = ON ? M::WF_Q(W) : 0, NB = ON ? M::WB_Q(W) : 0, NX = (ON && BWD) ? M::WX_Q(W) : 0;
+  static constexpr bool NEED_F = NEED_F_;   // a stored-activation RK4 backward never runs the forward
+  static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
+  static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
   f4 wf[NF > 0 ? NF : 1], wb[NB > 0 ? NB : 1], wx[NX > 0 ? NX : 1];
   __device__ __forceinline__ void load(Rsrc rs, int lane) {
     if constexpr (ON) {
       const int g = lane >> 4;
       sfor<M::D>([&](auto dd) {
         constexpr int d = decltype(dd)::value;
-        sfor<M::FT(d)>([&](auto kk) {
+        if constexpr (NEED_F) sfor<M::FT(d)>([&](auto kk) {
           constexpr int k = decltype(kk)::value;
           if constexpr (M::fowner(d, k) == W) {
             constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
@@ -392,6 +394,15 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
 
+// Stored activations (Model::STORE_ACT) of one tile-stage: [16][ACT_A4] behind the checkpoint.
+template <class M>
+__device__ __forceinline__ float* act_block(float* ckpt, int n_tiles, int n_steps, int tile, int step, int stage) {
+  const size_t ck = (size_t)n_tiles * n_steps * 4 * M::F * TT;
+  return ckpt + ck + (((size_t)tile * n_steps + step) * 4 + stage) * TT * M::ACT_A4;
+}
+template <class M>
+constexpr int act_q_per_thread() { return (TT * M::ACT_A4 / 4 + NTHREADS - 1) / NTHREADS; }
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -456,6 +467,20 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
         mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
+        if constexpr (TRAIN && M::STORE_ACT) {
+          // this stage's activation rows -> HBM for the backward (read before the flux barrier;
+          // the stores drain behind the rest of the stage)
+          f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
+          constexpr int QR = M::ACT_A4 / 4;
+          #pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * QR) {
+              const int t = i / QR, q = i - t * QR;
+              dst[i] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+            }
+          }
+        }
         sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
@@ -1079,7 +1104,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       });
     }
     __syncthreads();
-    static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
+    if constexpr (!M::STORE_ACT) static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     __syncthreads();
@@ -1114,14 +1139,41 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // stage input: from the staging slot the previous stage's flux pass filled,
         // or (first stage of the tile) straight from the forward's checkpoint
         if (have_next) {
-          constexpr int NV = TT * (M::F4 / 4);
+          // the 3R stage-input features (quads of the F4-wide staging row, clipped to the
+          // record's F16-wide Y slot: beyond it starts the activation region)
+          constexpr int QY = cmin(M::F4, M::F16) / 4, NV = TT * QY;
           #pragma unroll 1
           for (int i = tid; i < NV; i += NTHREADS) {
-            const int t = i / (M::F4 / 4), v = i - t * (M::F4 / 4);
+            const int t = i / QY, v = i - t * QY;
             *reinterpret_cast<f4*>(lds + t * SR + M::Y_OFF + 4 * v) =
                 *reinterpret_cast<const f4*>(lds + M::STG_LDS + t * M::F4 + 4 * v);
           }
+          if constexpr (M::STORE_ACT) {
+            constexpr int QR = M::ACT_A4 / 4;
+            #pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * QR) {
+                const int t = i / QR, q = i - t * QR;
+                *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) =
+                    *reinterpret_cast<const f4*>(lds + M::ACT_STG + 4 * i);
+              }
+            }
+          }
         } else {
+          if constexpr (M::STORE_ACT) {
+            // first stage of the tile: its activations straight from the forward's store
+            constexpr int QR = M::ACT_A4 / 4;
+            const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj));
+            #pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * QR) {
+                const int t = i / QR, q = i - t * QR;
+                *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = src[i];
+              }
+            }
+          }
           float ck[SL][3];
           ckpt_issue<M>(A, tile, step, jj, ck);
           sfor<SL>([&](auto ss) {
@@ -1156,16 +1208,41 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         constexpr bool EARLY_CK = SL == 1;
         if (EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
-          if constexpr (decltype(dd)::value == (M::D > 2 ? 1 : 0))
-            if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
-        });
+        if constexpr (M::STORE_ACT) {
+          // the stage's activations are the forward's (staged above); the next stage's are
+          // fetched now and land in ACT_STG after the flux pass
+          f4 actn[act_q_per_thread<M>()];
+          if (have_next) {
+            constexpr int QR = M::ACT_A4 / 4;
+            const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, nstep, njj));
+            #pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * QR) actn[u] = src[i];
+            }
+          }
+          if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+          flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+          if (have_next) {
+            constexpr int QR = M::ACT_A4 / 4;
+            #pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * QR) *reinterpret_cast<f4*>(lds + M::ACT_STG + 4 * i) = actn[u];
+            }
+          }
+        } else {
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
+            if constexpr (decltype(dd)::value == (M::D > 2 ? 1 : 0))
+              if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+          });
+        }
 
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
         if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        if constexpr (!M::STORE_ACT) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (next_out) {
           out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);

@@ -118,6 +118,7 @@ struct Model {
   // RK-state vectors are 12 * ceil(R/4) wide: the flux backward works on groups of
   // 4 regions (12 features) with 16-B LDS ops; QW = the matching width of the rates
   static constexpr int F4 = 12 * ((R + 3) / 4);
+  static constexpr int SLOTS_ = (R * TT + NTHREADS - 1) / NTHREADS;   // == SLOTS
   static constexpr int QW = 8 * ((R + 3) / 4);
   static constexpr int RK_A = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);  // adjoint of y_{n+1} (carried across steps)
   static constexpr int RK_PEND = RK_A + F4;       // y_n-side share of interpolated outputs
@@ -145,7 +146,18 @@ struct Model {
   static constexpr int STG_LDS = DB_LDS + (BAYES ? 2 : 1) * NDB;
   // SPLITX0: per-wave partial layer-0 input-gradient tiles [WAVES][XT(0)][64 lanes][4]
   static constexpr int X0P_LDS = STG_LDS + TT * F4;
-  static constexpr int LDS_B = (X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0)) * 4;
+  // ---- stored activations (small models) ----------------------------------------------
+  // At one tile per CU the backward's per-stage recompute of the forward (4 layer phases, each
+  // a barrier-separated latency chain) costs more than streaming the activations through HBM:
+  // the training forward writes each stage's activation rows [ACT0, ACT_END) of the record
+  // ([tile][step][stage][16][ACT_A4], behind the stage checkpoint) and the backward stages them
+  // back one stage ahead (ACT_STG) instead of recomputing.  288 GB of HBM makes this cheap:
+  // 7.7 GB for the 4096 x 365-step north-star solve.
+  static constexpr int ACT_A = ACT_END - ACT0;
+  static constexpr int ACT_A4 = (ACT_A + 3) & ~3;
+  static constexpr bool STORE_ACT = SLOTS_ == 1 && !BAYES && ACT_A4 <= 512;
+  static constexpr int ACT_STG = X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0);
+  static constexpr int LDS_B = (ACT_STG + (STORE_ACT ? TT * ACT_A4 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");
 
   // ---- packed weights (fragment order, 16-B per lane per MFMA quad) --------------

@@ -114,7 +114,16 @@ class _OdeintAdjoint(torch.autograd.Function):
                 n = torch.max(n, _mixed_norm(ap))
             return n
 
+        # the RHS appends to its tracking lists on every call (lib/models.py:137, :252); the
+        # augmented evaluations of the backward are not part of any loss, so their entries are
+        # dropped again (thousands of (N, R, 5) tensors per backward otherwise)
+        lists = [getattr(func, n) for n in ("params", "tracker") if isinstance(getattr(func, n, None), list)]
+        lens = [len(x) for x in lists]
+
+        counts = {"evals": 0}
+
         def augmented_dynamics(tt, y_aug):
+            counts["evals"] += 1
             yy, adj_y = y_aug[1], y_aug[2]
             with torch.enable_grad():
                 t_ = tt.detach().requires_grad_(True)
@@ -122,6 +131,8 @@ class _OdeintAdjoint(torch.autograd.Function):
                 # no gradient wrt time unless t requires it (torchdiffeq: func(t if t_requires_grad else t_, y))
                 func_eval = func(t_ if t_requires_grad else tt.detach(), yv)
                 grads = torch.autograd.grad(func_eval, (t_, yv) + adjoint_params, -adj_y, allow_unused=True)
+            for lst, n in zip(lists, lens):
+                del lst[n:]
             vjp_t, vjp_y, *vjp_params = grads
             vjp_t = torch.zeros_like(tt) if vjp_t is None else vjp_t
             vjp_y = torch.zeros_like(yy) if vjp_y is None else vjp_y
@@ -146,6 +157,10 @@ class _OdeintAdjoint(torch.autograd.Function):
                 aug_state[2] = aug_state[2] + grad_y[i - 1]
             if t_requires_grad:
                 time_vjps[0] = -aug_state[0]
+        try:
+            func.last_adjoint_info = {"augmented_evals": counts["evals"], "seminorm": seminorm}
+        except AttributeError:
+            pass
         adj_y = aug_state[2]
         adj_params = aug_state[3:]
         return (None, adj_y, time_vjps, None, None, None, None, None, None, None, None, None, *adj_params)

@@ -84,7 +84,13 @@ def _rms_default(x: torch.Tensor) -> torch.Tensor:
 
 
 def _dot(ks: List[torch.Tensor], c: torch.Tensor) -> torch.Tensor:
-    return torch.stack(ks, -1).matmul(c)
+    """sum_i c[i] * ks[i] (torchdiffeq: ``stack(k, -1).matmul(c)``) as a chain of multiply-adds:
+    the (n, k) x (k,) matmul is a transposed GEMV that rocBLAS runs with one workgroup per
+    output element -- 11 ms for a 10^6-element augmented adjoint state, vs ~20 us here."""
+    acc = ks[0] * c[0]
+    for i in range(1, len(ks)):
+        acc = torch.addcmul(acc, ks[i], c[i])
+    return acc
 
 
 def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,

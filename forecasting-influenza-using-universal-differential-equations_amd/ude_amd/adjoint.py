@@ -71,7 +71,11 @@ def _solve_segment(aug_func, flat: _Flat, state: List[torch.Tensor], t_from, t_t
     s_pair = torch.stack([-t_from, -t_to])
 
     def f_rev(s, yf):
-        return -flat.flat(aug_func(-s, flat.split(yf)))
+        # the negated pieces written straight into one flat vector (no cat + negate pass)
+        out = torch.empty_like(yf)
+        for piece, view in zip(aug_func(-s, flat.split(yf)), flat.split(out)):
+            torch.neg(piece.reshape(view.shape), out=view)
+        return out
 
     opts = dict(options or {})
     if method == "dopri5":

@@ -17,6 +17,8 @@ reference's draws).
 """
 from __future__ import annotations
 
+import contextlib
+
 import math
 from typing import List, Optional, Tuple
 
@@ -121,10 +123,21 @@ class _BayesBase(_UDEModule):
             sds += [lay.w_std, lay.b_std]
         return mus, sds
 
-    def _eval_weights(self) -> List[torch.Tensor]:
+    def ude_weight_shapes(self) -> List[torch.Size]:
+        return [p.shape for p in self.ude_mean_std()[0]]
+
+    def _eval_weights(self):
         """This evaluation's weight sample, drawn and formed by the layers exactly as their
         forward does (make_z per layer in call order; w = mean + z * |std|, :43-48) -- or, with
-        a stream set by ``set_eps_stream``, its next row (torch parameter order per layer)."""
+        a stream set by ``set_eps_stream``, its next row (torch parameter order per layer) --
+        or, inside a fixed-grid solve (``presampled``), the next pre-formed sample row."""
+        pre = getattr(self, "_presampled", None)
+        if pre is not None:
+            k = self._pre_row
+            if k >= len(pre):
+                raise RuntimeError(f"presampled weights: evaluation {k + 1} of a solve drawn for {len(pre)}")
+            self._pre_row = k + 1
+            return pre[k]
         eps = getattr(self, "_eps_next", None)
         row = None
         if eps is not None:
@@ -150,6 +163,25 @@ class _BayesBase(_UDEModule):
         whole-solve kernel takes all of it, evaluations one at a time take a row each."""
         self._eps_next = eps
         self._eps_row = 0
+
+    @contextlib.contextmanager
+    def presampled(self, n_eval: int, device):
+        """Draw the weight samples of a whole solve's ``n_eval`` evaluations at once --
+        ``w = mean + eps * |std|`` on the (n_eval, n_params) stream ``take_eps`` hands the
+        fused whole-solve kernel (same rows, same fp32 ops as one evaluation at a time) -- and
+        serve evaluation e row e.  Three device operators per solve instead of four per layer
+        per evaluation, and one gradient reduction over the rows instead of an accumulation
+        per evaluation (autograd: mean and std receive the row gradients through the stack)."""
+        mus, sds = self.ude_mean_std()
+        n_par = sum(int(p.numel()) for p in mus)
+        eps = self.take_eps(n_eval, n_par, device)
+        mu = torch.cat([p.reshape(-1) for p in mus])
+        sd = torch.cat([p.reshape(-1) for p in sds])
+        self._presampled, self._pre_row = (mu + eps * torch.abs(sd)).unbind(0), 0
+        try:
+            yield
+        finally:
+            self._presampled = None
 
     def take_eps(self, n_eval: int, n_params: int, device) -> torch.Tensor:
         eps = getattr(self, "_eps_next", None)

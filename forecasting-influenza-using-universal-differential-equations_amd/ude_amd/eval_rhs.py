@@ -56,14 +56,27 @@ def _plan(cfg, n: int, fa_w: float, device: torch.device) -> _Plan:
 
 class _FusedEval(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, plan: _Plan, x: torch.Tensor, *wb: torch.Tensor):
+    def forward(ctx, plan: _Plan, shapes, x: torch.Tensor, *wb: torch.Tensor):
+        """``shapes`` None: wb = (W, b) per Linear; else wb = (one flat weight vector,) holding
+        the tensors of ``shapes`` back to back (C-ABI order), whose gradient comes back flat."""
         dev = x.device
         stream = _fused._stream(dev)
         N, R, L = x.shape
-        ws_ = [w.contiguous() for w in wb[0::2]]
-        bs_ = [b.contiguous() for b in wb[1::2]]
+        if shapes is None:
+            ws_ = [w.contiguous() for w in wb[0::2]]
+            bs_ = [b.contiguous() for b in wb[1::2]]
+            ptrs = [t.data_ptr() for t in ws_], [t.data_ptr() for t in bs_]
+        else:
+            flat = wb[0].contiguous()
+            offs, off = [], 0
+            for shp in shapes:
+                offs.append(flat.data_ptr() + 4 * off)
+                off += int(torch.Size(shp).numel())
+            if off != flat.numel() or flat.dtype != torch.float32:
+                raise ValueError(f"flat weights: {flat.numel()} {flat.dtype} elements, the model has {off} fp32")
+            ptrs = offs[0::2], offs[1::2]
         pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
-        plan.lib.pack(plan.desc, [w.data_ptr() for w in ws_], [b.data_ptr() for b in bs_], pack.data_ptr(), stream)
+        plan.lib.pack(plan.desc, ptrs[0], ptrs[1], pack.data_ptr(), stream)
         x = x.contiguous()
         f = torch.empty_like(x)
         rates = torch.empty((N, R, 2), dtype=torch.float32, device=dev) if plan.has_p else x.new_empty(0)
@@ -71,6 +84,7 @@ class _FusedEval(torch.autograd.Function):
         plan.lib.rhs_forward(plan.desc, plan.prob, pack.data_ptr(), x.data_ptr(), f.data_ptr(),
                              rates.data_ptr() if plan.has_p else None, fa.data_ptr() if plan.has_a else None, stream)
         ctx.plan = plan
+        ctx.flat = shapes is not None
         ctx.shapes = [t.shape for t in wb]
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, pack)
@@ -83,7 +97,7 @@ class _FusedEval(torch.autograd.Function):
         dev = x.device
         n_wb = len(ctx.shapes)
         if gf is None and grates is None and gfa is None:
-            return (None, None) + (None,) * n_wb
+            return (None, None, None) + (None,) * n_wb
         gf = torch.zeros_like(x) if gf is None else gf.contiguous().float()
         grates = None if (grates is None or not plan.has_p) else grates.contiguous().float()
         gfa = None if (gfa is None or not plan.has_a) else gfa.contiguous().float()
@@ -94,7 +108,9 @@ class _FusedEval(torch.autograd.Function):
             plan.lib.rhs_vjp(plan.desc, plan.prob, pack.data_ptr(), x.data_ptr(), gf.data_ptr(),
                              None if grates is None else grates.data_ptr(), None if gfa is None else gfa.data_ptr(),
                              dx.data_ptr(), ws.data_ptr(), dparams.data_ptr(), _fused._stream(dev))
-        return (None, dx) + tuple(_fused._split(dparams, ctx.shapes))
+        if ctx.flat:
+            return None, None, dx, dparams
+        return (None, None, dx) + tuple(_fused._split(dparams, ctx.shapes))
 
 
 def eligible(module, x: torch.Tensor) -> bool:
@@ -110,11 +126,15 @@ def deterministic_config(module):
     return (kind[1:] if kind.startswith("B") else kind, R, L, net, aug)
 
 
-def rhs_eval(module, x: torch.Tensor, weights: Sequence[torch.Tensor]
+def rhs_eval(module, x: torch.Tensor, weights
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
     """(f, rates, Fa) of one evaluation; weights = (W, b) per Linear in C-ABI order (rate net
-    first).  rates / Fa are None for the net the module does not have."""
+    first), or those tensors back to back in one 1-D tensor (a pre-drawn Bayesian sample row).
+    rates / Fa are None for the net the module does not have."""
     plan = _plan(deterministic_config(module), x.shape[0], module.fa_weight(), x.device)
     with torch.cuda.device(x.device):
-        f, rates, fa = _FusedEval.apply(plan, x, *weights)
+        if isinstance(weights, torch.Tensor):
+            f, rates, fa = _FusedEval.apply(plan, module.ude_weight_shapes(), x, weights)
+        else:
+            f, rates, fa = _FusedEval.apply(plan, None, x, *weights)
     return f, (rates if plan.has_p else None), (fa if plan.has_a else None)

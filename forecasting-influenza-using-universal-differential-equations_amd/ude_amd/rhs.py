@@ -189,6 +189,13 @@ class _UDEModule(nn.Module):
     def fa_weight(self) -> float:
         return float(getattr(self, "Fa_w", 1.0))
 
+    def ude_weight_shapes(self) -> List[torch.Size]:
+        """Shapes of (W, b) per Linear in C-ABI order."""
+        out: List[torch.Size] = []
+        for lin in self.ude_linears():
+            out += [lin.weight.shape, lin.bias.shape]
+        return out
+
     def _eval_weights(self) -> List[torch.Tensor]:
         out: List[torch.Tensor] = []
         for lin in self.ude_linears():

@@ -170,6 +170,7 @@ def _step_midpoint(func, t0, dt, t1, y):
 
 
 _STEPS = {"rk4": _step_rk4, "euler": _step_euler, "midpoint": _step_midpoint}
+_STAGES = {"rk4": 4, "euler": 1, "midpoint": 2}
 
 
 def eager_fixed_grid(func, y0, t, method="rk4", step_size=None):
@@ -224,4 +225,10 @@ def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, even
     if isinstance(func, _UDEModule) and _strict() and not _eval_fused(func, y0):
         raise RuntimeError("UDE_STRICT=1: this solve would not run on the fused gfx950 kernels "
                            f"(method={method}, device={y0.device}, dtype={y0.dtype})")
+    if getattr(func, "uncertainty", None) == "bayes" and _eval_fused(func, y0):
+        # Bayesian RHS evaluated one kernel per evaluation: the whole solve's weight samples
+        # are formed up front (the whole-solve kernel's eps stream, ude_amd/bayes.py)
+        n_eval = (len(fixed_grid(t, step_size)) - 1) * _STAGES[method]
+        with func.presampled(n_eval, y0.device):
+            return eager_fixed_grid(func, y0, t, method, step_size)
     return eager_fixed_grid(func, y0, t, method, step_size)

@@ -15,7 +15,7 @@ Outputs (npz, no pickles): inputs, eps, weights, the fp64 reference outputs and
 the VJP of a fixed linear functional w.r.t. y0 and every parameter (means and
 stds), and the reference's own fp32-vs-fp64 distances.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_bayes.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_bayes.py [case names]
 """
 from __future__ import annotations
 
@@ -43,6 +43,8 @@ CASES = [
     ("bayes_fa_r1_weekly", "Fa", 1, 8, None, [32, 32], 20, ("arange", 6, 1.0), "t1-t0", 1.0),
     ("bayes_fafp_r1_interp", "FaFp", 1, 8, [64, 64, 32], [64, 64], 33, ("linspace", 12, 7.0), 0.25, 0.5),
     ("bayes_fafp_r10_weekly", "FaFp", 10, 8, [64, 64, 32], [64, 64], 18, ("arange", 4, 1.0), "t1-t0", 1.0),
+    # the state model's size ('UONNb', run_ode.py): beyond the fused whole-solve kernel
+    ("bayes_fafp_r49_weekly", "FaFp", 49, 8, [64, 64, 32], [64, 64], 10, ("arange", 3, 1.0), "t1-t0", 1.0),
 ]
 
 
@@ -120,9 +122,11 @@ def run(mod, eps, y0, t, step, dlatent, dmean, dstd, dnorm, dtype):
     return out
 
 
-def main():
+def main(only=None):
     torch.set_num_threads(1)
     for ci, (name, kind, R, L, net, aug, N, tspec, step, fa_w) in enumerate(CASES):
+        if only and name not in only:
+            continue
         torch.manual_seed(3000 + ci)
         gen = torch.Generator().manual_seed(4000 + ci)
         mod = build(kind, R, L, net, aug)
@@ -169,4 +173,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -274,7 +274,7 @@ def loss_head_line(pkg, w, dev, reps=20):
                          "algorithmic_bytes": {"fwd": lat_bytes, "bwd": 2 * lat_bytes}}}
 
 
-def adjoint_line(pkg, w, dev, T=2, rtol=1e-5, atol=1e-7, seminorm=True):
+def adjoint_line(pkg, w, dev, T=2, rtol=1e-5, atol=1e-7, seminorm=True, reps=2):
     """BASELINE configs[2] forward + adjoint backward on the state49 batch: odeint_adjoint
     (torchdiffeq semantics) -- forward = the fused dopri5 solve, backward = the augmented
     dopri5 solve whose every evaluation is the gfx950 evaluation + VJP kernels."""
@@ -295,11 +295,13 @@ def adjoint_line(pkg, w, dev, T=2, rtol=1e-5, atol=1e-7, seminorm=True):
         info.update(mod.last_adjoint_info)
         return info
 
+    step()                              # warm-up: evaluation plans, kernel attributes, allocator
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    info = step()
+    for _ in range(reps):
+        info = step()
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    el = (time.perf_counter() - t0) / reps
     return {"workload": f"state49 batch ({w['n_traj']} trajectories, R=49), t = {T - 1} weekly interval(s), "
                         f"odeint_adjoint dopri5 rtol {rtol:g} atol {atol:g}"
                         f"{' adjoint_options norm=seminorm' if seminorm else ''}, forward + adjoint backward",

@@ -235,7 +235,7 @@ struct Ops {
       HIPCHK(hipGetLastError());
     }
     if (M::HOIST) {
-      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS, M::STATIC_GROUPS), dim3(256), 0, s,
                          (const float*)g0buf, y0, p->n_traj, n_tiles, part);
       HIPCHK(hipGetLastError());
       hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
@@ -534,7 +534,7 @@ struct EvalOps {
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());
     if (M::HOIST) {
-      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS), dim3(256), 0, s,
+      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS, M::STATIC_GROUPS), dim3(256), 0, s,
                          (const float*)g0buf, x, p->n_traj, n_tiles, part);
       HIPCHK(hipGetLastError());
       hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,

@@ -1624,56 +1624,49 @@ __global__ __launch_bounds__(256) void ude_eps_slab_kernel(const float* __restri
 // ============================================================================
 // dW0[:, static] split-K partials on MFMA: part[chunk][K0][S16] = sum over the
 // chunk's tiles of G0[tile] (K0 x 16 trajectories) x X_static[tile] (16 x S16).
-// Wave w owns static column tiles w, w + 4, ...; MFMA q covers trajectories 4g + q.
+// Grid (STATIC_CHUNKS, STATIC_GROUPS): wave w of column group y owns static column tile
+// 4y + w (every wave of the chip busy: the K0 x S16 x N GEMM is MFMA-issue bound);
+// MFMA q covers trajectories 4g + q.  Tiles are walked two at a time so the next tile's
+// operand loads are in flight during this tile's MFMAs.
 template <class M>
 __global__ __launch_bounds__(256) void ude_static_partial_kernel(const float* __restrict__ g0buf,
                                                                  const float* __restrict__ y0, int n_traj,
                                                                  int n_tiles, float* __restrict__ part) {
-  constexpr int NOT = M::K0 / 16, NST = M::S16 / 16, SPW = (NST + 3) / 4;
+  constexpr int NOT = M::K0 / 16, NST = M::S16 / 16;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int st = blockIdx.y * 4 + w;
+  if (st >= NST) return;                             // no barriers or LDS in this kernel
   const int chunk = blockIdx.x;
   const int per = (n_tiles + M::STATIC_CHUNKS - 1) / M::STATIC_CHUNKS;
   const int tb = chunk * per, te = min(n_tiles, tb + per);
-  f4 acc[NOT][SPW];
+  const int s = st * 16 + t;
+  const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
+  const bool s_ok = s < M::S;
+  f4 acc[NOT];
 #pragma unroll
-  for (int o = 0; o < NOT; ++o)
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) acc[o][j] = f4zero();
-  #pragma unroll 1
+  for (int o = 0; o < NOT; ++o) acc[o] = f4zero();
+  #pragma unroll 2
   for (int tile = tb; tile < te; ++tile) {
     f4 a[NOT];
 #pragma unroll
     for (int o = 0; o < NOT; ++o)
       a[o] = *reinterpret_cast<const f4*>(g0buf + ((size_t)tile * M::K0 + o * 16 + t) * TT + 4 * g);
-    float b[SPW][4];
+    float b[4];
 #pragma unroll
-    for (int j = 0; j < SPW; ++j) {
-      const int s = (w + 4 * j) * 16 + t;
-      const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = tile * TT + 4 * g + q;
-        b[j][q] = (s < M::S && n < n_traj) ? y0[((size_t)n * M::R + r) * M::L + 3 + cc] : 0.f;
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int n = tile * TT + 4 * g + q;
+      b[q] = (s_ok && n < n_traj) ? y0[((size_t)n * M::R + r) * M::L + 3 + cc] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int j = 0; j < SPW; ++j)
-        if (w + 4 * j < NST)
-#pragma unroll
-          for (int o = 0; o < NOT; ++o) acc[o][j] = mfma4(a[o][q], b[j][q], acc[o][j]);
+      for (int o = 0; o < NOT; ++o) acc[o] = mfma4(a[o][q], b[q], acc[o]);
   }
 #pragma unroll
-  for (int j = 0; j < SPW; ++j) {
-    const int st = w + 4 * j;
-    if (st >= NST) continue;
+  for (int o = 0; o < NOT; ++o)
 #pragma unroll
-    for (int o = 0; o < NOT; ++o)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        part[((size_t)chunk * M::K0 + o * 16 + 4 * g + e) * M::S16 + st * 16 + t] = acc[o][j][e];
-  }
+    for (int e = 0; e < 4; ++e)
+      part[((size_t)chunk * M::K0 + o * 16 + 4 * g + e) * M::S16 + st * 16 + t] = acc[o][e];
 }
 
 template <class M>
@@ -1742,15 +1735,33 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
   __syncthreads();
   const float* gb = g0buf + (size_t)tile * M::K0 * TT;
   const float* wp = pack + M::W0SP_OFF;
+  // operands in batches of QB k-steps, loaded unconditionally (column tiles past NST clamp
+  // to the last one; their results are never stored) so a batch's loads are all in flight
+  // before its MFMAs -- a guarded load per MFMA serialises on its latency
+  constexpr int KQ = M::K0 / 4, QB = 8;
+  int col[SPW];
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) col[j] = min(w + 4 * j, NST - 1) * 16 + t;
   f4 acc[SPW];
 #pragma unroll
   for (int j = 0; j < SPW; ++j) acc[j] = f4zero();
-#pragma unroll 8
-  for (int q = 0; q < M::K0 / 4; ++q) {
-    const float a = gb[(4 * q + g) * TT + t];          // A[traj t][o = 4q + g]
 #pragma unroll
-    for (int j = 0; j < SPW; ++j)
-      if (w + 4 * j < NST) acc[j] = mfma4(a, wp[(4 * q + g) * M::S16 + (w + 4 * j) * 16 + t], acc[j]);
+  for (int q0 = 0; q0 < KQ; q0 += QB) {
+    float a[QB], b[QB][SPW];
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+      if (q0 + qq < KQ) {
+        const int k = 4 * (q0 + qq) + g;
+        a[qq] = gb[k * TT + t];                        // A[traj t][o = k]
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) b[qq][j] = wp[k * M::S16 + col[j]];
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq)
+      if (q0 + qq < KQ)
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) acc[j] = mfma4(a[qq], b[qq][j], acc[j]);
   }
 #pragma unroll
   for (int j = 0; j < SPW; ++j) {

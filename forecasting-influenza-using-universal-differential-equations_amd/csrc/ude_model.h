@@ -210,6 +210,7 @@ struct Model {
   // static-feature gradient work (outside the main kernel, HOIST only): per-tile
   // layer-0 row sums G0[tile][K0][16] and split-K partials of dW0[:, static]
   static constexpr int STATIC_CHUNKS = 128;
+  static constexpr int STATIC_GROUPS = (S16 / 16 + 3) / 4;
 
   // ---- per-wave register tiles -----------------------------------------------------
   static constexpr int ndw_before(int w, int d, int k) {

@@ -1007,6 +1007,20 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
         RkAdjointEp<M, SR>{rec, dt, jj}(f0 + 4 * v, dY);
       }
     }
+    // the padded rows of the final-layer gradient slots (the slots alias wider layers'
+    // gradients, so they are re-zeroed every stage), by the item of the last region group
+    if (rg == RG - 1) {
+      if constexpr (M::HAS_P) {
+        constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
+#pragma unroll
+        for (int o = lo; o < hi; o += 4) *reinterpret_cast<f4*>(rec + QG + o) = f4zero();
+      }
+      if constexpr (M::HAS_A) {
+        constexpr int lo = cmin(M::F4, M::kout(1, M::nl(1) - 1)), hi = M::kout(1, M::nl(1) - 1);
+#pragma unroll
+        for (int o = lo; o < hi; o += 4) *reinterpret_cast<f4*>(rec + FG + o) = f4zero();
+      }
+    }
   }
 }
 
@@ -1111,6 +1125,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     UDE_STAMP(pf, 15);
 
     bool have_next = false;
+    // small records with stored activations (CARRY): the next stage's activation rows and
+    // checkpointed input are loaded into registers one whole stage ahead and written
+    // straight into the record at that stage's start (no LDS staging slot, and the HBM
+    // latency is covered by a full stage of work instead of one flux pass)
+    constexpr bool CARRY = M::STORE_ACT && SL == 1;
+    f4 actr[CARRY ? act_q_per_thread<M>() : 1];
+    float ckr[SL][3];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's
@@ -1138,7 +1159,22 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         // stage input: from the staging slot the previous stage's flux pass filled,
         // or (first stage of the tile) straight from the forward's checkpoint
-        if (have_next) {
+        if (CARRY && have_next) {
+          constexpr int QR = M::ACT_A4 / 4;
+#pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * QR) {
+              const int t = i / QR, q = i - t * QR;
+              *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = actr[u];
+            }
+          }
+          if (tid < M::PAIRS) {
+            const int r = tid / TT, t = tid - r * TT;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = ckr[0][c];
+          }
+        } else if (have_next) {
           // the 3R stage-input features (quads of the F4-wide staging row, clipped to the
           // record's F16-wide Y slot: beyond it starts the activation region)
           constexpr int QY = cmin(M::F4, M::F16) / 4, NV = TT * QY;
@@ -1207,8 +1243,26 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // wide ones under the flux pass (registers only live across that pass)
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         constexpr bool EARLY_CK = SL == 1;
-        if (EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        if constexpr (M::STORE_ACT) {
+        if constexpr (CARRY) {
+          // output cotangent loads first: out_finish below waits for them with the carried
+          // loads (issued after) still in flight
+          if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+          if (have_next) {
+            ckpt_issue<M>(A, tile, nstep, njj, ckr);
+            constexpr int QR = M::ACT_A4 / 4;
+            const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, nstep, njj));
+#pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * QR) actr[u] = src[i];
+            }
+          }
+          flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        } else if (EARLY_CK && have_next) {
+          ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        }
+        if constexpr (CARRY) {
+        } else if constexpr (M::STORE_ACT) {
           // the stage's activations are the forward's (staged above); the next stage's are
           // fetched now and land in ACT_STG after the flux pass
           f4 actn[act_q_per_thread<M>()];
@@ -1262,7 +1316,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 17);
-        if (have_next) {
+        if (!CARRY && have_next) {
           sfor<SL>([&](auto ss) {
             constexpr int sl = decltype(ss)::value;
             const int p = tid + sl * NTHREADS;
@@ -1274,23 +1328,6 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 18);
-        // zero the padded rows of the final-layer gradient slots
-        if constexpr (M::HAS_P) {
-          constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
-          #pragma unroll 1
-          for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
-            const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
-            lds[t * SR + M::gbuf(0, M::nl(0) - 1) + o] = 0.f;
-          }
-        }
-        if constexpr (M::HAS_A) {
-          constexpr int lo = cmin(M::F4, M::kout(1, M::nl(1) - 1)), hi = M::kout(1, M::nl(1) - 1);
-          #pragma unroll 1
-          for (int i = tid; i < TT * (hi - lo); i += NTHREADS) {
-            const int t = i / (hi - lo), o = lo + i - t * (hi - lo);
-            lds[t * SR + M::gbuf(1, M::nl(1) - 1) + o] = 0.f;
-          }
-        }
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);

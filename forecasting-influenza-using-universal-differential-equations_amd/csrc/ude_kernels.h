@@ -672,7 +672,65 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       });
     }
     __builtin_amdgcn_sched_barrier(0);
-    // (1) rows owned by this wave: bias/G sums and the dW GEMM (K = trajectories)
+    // (1) rows owned by this wave: bias/G sums and the dW GEMM (K = trajectories).
+    // When they fit, every owned tile's LDS operands are read before the first MFMA
+    // (one LDS latency per phase instead of one per tile).
+    constexpr int NOWN = M::own_phase(W, d);
+    constexpr int NDP = M::ndw_phase(W, d);
+    constexpr bool BATCH = !M::BAYES && NOWN > 0 && 4 * NOWN * 2 + 4 * NDP <= 96;
+    if constexpr (BATCH) {
+      f4 gvv[NOWN];
+      float gaa[NOWN][4], bva[NDP][4];
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          constexpr int net = M::fnet(d, k), rt = M::frt(d, k), goff = M::gbuf(net, d);
+          constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
+          constexpr int o = M::ng_before(W, d, k) - M::ng_before(W, d, 0);
+          constexpr int e0 = M::ndw_before(W, d, k) - M::ndw_before(W, d, 0);
+          gvv[o] = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            gaa[o][s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
+            sfor<M::rti(net, d)>([&](auto cc) {
+              constexpr int ct = decltype(cc)::value;
+              bva[e0 + ct][s] = lds[(4 * g + s) * SR + inoff + ct * 16 + t];
+            });
+          }
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          constexpr int net = M::fnet(d, k);
+          constexpr int o = M::ng_before(W, d, k) - M::ng_before(W, d, 0);
+          constexpr int e0 = M::ndw_before(W, d, k) - M::ndw_before(W, d, 0);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            sfor<M::rti(net, d)>([&](auto cc) {
+              constexpr int ct = decltype(cc)::value;
+              constexpr int idx = M::ndw_before(W, d, k) + ct;
+              dw[idx] = mfma4(gaa[o][s], bva[e0 + ct][s], dw[idx]);
+            });
+          if constexpr (d == 0) {
+            g0t[M::nz_before(W, k)] += gvv[o];
+          } else {
+            f4 r = gvv[o];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+              r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+            }
+            if (t == 0) {
+              float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
+              db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+            }
+          }
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    } else
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
@@ -771,9 +829,18 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       UDE_STAMP(pf, 7 + d);
       return;
     }
+    f4 avv[M::XT(d) > 0 ? M::XT(d) : 1];
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
-      if constexpr (M::xowner(d, m) == W) xa[m] = f4zero();
+      if constexpr (M::xowner(d, m) == W) {
+        xa[m] = f4zero();
+        if constexpr (d > 0) {
+          // the ELU-derivative operand of the epilogue, read ahead of the MFMAs
+          constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
+          if constexpr (M::act(net, d - 1))
+            avv[m] = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
+        }
+      }
     });
     sfor<2>([&](auto nn) {
       constexpr int net = decltype(nn)::value;
@@ -809,7 +876,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
           constexpr int net = M::xnet(d, m);
           constexpr int rt = M::xrt(d, m);
           if constexpr (M::act(net, d - 1)) {
-            const f4 av = *reinterpret_cast<const f4*>(rec + M::act_off(net, d - 1) + rt * 16 + g * 4);
+            const f4 av = avv[m];
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[e] = av[e] <= 0.f ? acc[e] * (av[e] + 1.f) : acc[e];
           }

@@ -244,6 +244,11 @@ struct Model {
     return s;
   }
   static constexpr int NG(int w) { return ng_before(w, D, 0); }
+  static constexpr int own_phase(int w, int d) {
+    int s = 0;
+    for (int k = 0; k < FT(d); ++k) if (fowner(d, k) == w) s += 1;
+    return s;
+  }
   static constexpr int nz_before(int w, int k) {
     int s = 0;
     for (int kk = 0; kk < k; ++kk) if (fowner(0, kk) == w) s += 1;

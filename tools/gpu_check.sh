@@ -14,6 +14,7 @@ if [ "$1" = "prof" ]; then
   cat gpurun_out/stage_m1.txt
   timeout -k 10 120 python -u tools/stage_profile.py state49 > gpurun_out/stage_s49.txt 2>&1 || exit $?
   cat gpurun_out/stage_s49.txt
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_m1 -o m1 -- python3 bench.py --workload us_northstar --steps 5 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/prof_m1.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_m1 -o m1 -- python3 bench.py --workload us_northstar --steps 5 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/prof_m1.log 2>&1 || exit $?
+  find /tmp/prof_m1 -name "*kernel_stats.csv" -exec cp {} gpurun_out/m1_kernel_stats.csv \;
 fi
 exit $rc

@@ -368,9 +368,11 @@ struct LossOps {
   struct Layout {
     size_t musd, part, slab, total;
   };
-  static int grid(int device, int T, int S, int B, int* g) {
+  // forward and backward grids differ (the forward needs no decoder-weight copy in LDS: two
+  // workgroups per CU); the workspace holds the forward's partials and the backward's slabs
+  static int grid(int device, int T, int S, int B, bool bwd, int* g) {
     if (T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
-    const int lds = D::lds_bytes(S);
+    const int lds = D::lds_bytes(S, bwd);
     if (lds > 160 * 1024 || pad16(S) > SP_MAX) return UDE_E_UNSUPPORTED;
     static bool done = false;
     if (!done) {
@@ -380,26 +382,34 @@ struct LossOps {
     }
     int cus = 0, occ = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, true>, LTHREADS, lds));
+    if (bwd)
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, true>, LTHREADS, lds));
+    else
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_loss_kernel<D, M::L, false>, LTHREADS, lds));
     if (occ < 1) occ = 1;
     const long mx = (long)cus * occ, groups = (long)T * B;
     *g = (int)(groups < mx ? groups : mx);
     return UDE_OK;
   }
-  static Layout layout(int T, int B, int g) {
+  static Layout layout(int T, int B, int gf, int gb) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     Layout L;
     L.musd = 0;
     L.part = al((size_t)T * B * M::R * 2 * 4);
-    L.slab = L.part + al((size_t)g * 2 * 8);
-    L.total = L.slab + al((size_t)g * D::SLAB * 4);
+    L.slab = L.part + al((size_t)gf * 2 * 8);
+    L.total = L.slab + al((size_t)gb * D::SLAB * 4);
     return L;
   }
-  static int workspace(int T, int S, int B, int device, int64_t* bytes) {
-    int g = 1;
-    int rc = grid(device, T, S, B, &g);
+  static int grids(int device, int T, int S, int B, int* gf, int* gb) {
+    int rc = grid(device, T, S, B, false, gf);
     if (rc) return rc;
-    *bytes = (int64_t)layout(T, B, g).total;
+    return grid(device, T, S, B, true, gb);
+  }
+  static int workspace(int T, int S, int B, int device, int64_t* bytes) {
+    int gf = 1, gb = 1;
+    int rc = grids(device, T, S, B, &gf, &gb);
+    if (rc) return rc;
+    *bytes = (int64_t)layout(T, B, gf, gb).total;
     return UDE_OK;
   }
   static int run(bool bwd, int T, int S, int B, const float* latent, const float* W, const float* b, const float* y,
@@ -408,10 +418,10 @@ struct LossOps {
     if (!latent || !W || !b || !y || !ws) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
-    int g = 1;
-    int rc = grid(dev, T, S, B, &g);
+    int gf = 1, gb = 1;
+    int rc = grids(dev, T, S, B, &gf, &gb);
     if (rc) return rc;
-    const Layout Lo = layout(T, B, g);
+    const Layout Lo = layout(T, B, gf, gb);
     unsigned char* base = (unsigned char*)ws;
     LArgs a;
     memset(&a, 0, sizeof(a));
@@ -419,20 +429,19 @@ struct LossOps {
     a.musd = (float*)(base + Lo.musd); a.part = (double*)(base + Lo.part); a.slab = (float*)(base + Lo.slab);
     a.dlatent = dlatent; a.grad = grad;
     a.T = T; a.S = S; a.B = B; a.dl_sir = dl_sir;
-    const int lds = D::lds_bytes(S);
     if (!bwd) {
       if (!out) return UDE_E_INVALID;
-      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, false>), dim3(g), dim3(LTHREADS), lds, s, a);
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, false>), dim3(gf), dim3(LTHREADS), D::lds_bytes(S, false), s, a);
       HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL(ude_loss_finalize_kernel<0>, dim3(1), dim3(128), 0, s, (const double*)a.part, g,
+      hipLaunchKernelGGL(ude_loss_finalize_kernel<0>, dim3(1), dim3(128), 0, s, (const double*)a.part, gf,
                          (double)B * T * M::R, out);
       HIPCHK(hipGetLastError());
     } else {
       if (!grad || !dlatent || !dW || !db) return UDE_E_INVALID;
-      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, true>), dim3(g), dim3(LTHREADS), lds, s, a);
+      hipLaunchKernelGGL((ude_loss_kernel<D, M::L, true>), dim3(gb), dim3(LTHREADS), D::lds_bytes(S, true), s, a);
       HIPCHK(hipGetLastError());
       hipLaunchKernelGGL((ude_loss_grad_finalize_kernel<D>), dim3((D::SLAB + 63) / 64), dim3(256), 0, s,
-                         (const float*)a.slab, g, dW, db);
+                         (const float*)a.slab, gb, dW, db);
       HIPCHK(hipGetLastError());
     }
     return UDE_OK;

@@ -30,10 +30,15 @@ struct LossDims {
   static constexpr int NTILE = NT * KT;      // dW tiles (16 x 16)
   static constexpr int tiles_of(int w) { return (NTILE + LWAVES - 1 - w) / LWAVES; }
   static constexpr int SLAB = NP * KP + NP;  // per-workgroup dW | db partials
-  static_assert(NP <= LTHREADS / 4, "one lane quad per decoder output");
-  static int lds_bytes(int S) {
+  static constexpr int LPR = 8;              // lanes per decoder output in the statistics pass
+  static_assert(NP <= LTHREADS / LPR, "one lane octet per decoder output");
+  // forward: each wave's GEMM tiles share one output-column tile (LWAVES % NT == 0), whose
+  // decoder-weight fragment (KP/4 floats per lane) stays in registers -- no weight copy in LDS,
+  // so two workgroups fit a CU
+  static constexpr bool FWD_WREG = LWAVES % NT == 0;
+  static int lds_bytes(int S, bool bwd = true) {
     const int SP = pad16(S);
-    return (SP * XS + NP * XS + SP * PS + 2 * NP) * 4;
+    return (SP * XS + ((bwd || !FWD_WREG) ? NP * XS : 0) + SP * PS + 2 * NP) * 4;
   }
 };
 
@@ -71,20 +76,34 @@ template <class D, int L, bool BWD, int W>
 __device__ void loss_body(const LArgs& A, float* lds) {
   const int tid = threadIdx.x, lane = tid & 63, t16 = lane & 15, g = lane >> 4;
   const int S = A.S, SP = pad16(S), N = A.S * A.B;
+  constexpr bool WF = !BWD && D::FWD_WREG;       // decoder weight in registers (forward)
   float* X = lds;
   float* Wl = X + SP * D::XS;
-  float* P = Wl + D::NP * D::XS;
+  float* P = WF ? Wl : Wl + D::NP * D::XS;
   float* bl = P + SP * D::PS;
   const size_t NRL = (size_t)N * D::R * L;
   const double M = (double)A.B * A.T * D::R;    // nll.mean() over (B, T, R)
   const float g_nll = BWD ? A.grad[0] : 0.f, g_reg = BWD ? A.grad[1] : 0.f;
   const int ngroups = A.T * A.B;
 
-  // decoder weight / bias -> LDS (zero padded), X padding zeroed, once per workgroup
-  #pragma unroll 1
-  for (int i = tid; i < D::NP * D::XS; i += LTHREADS) {
-    const int o = i / D::XS, k = i - o * D::XS;
-    Wl[i] = (o < D::R && k < D::K) ? A.W[o * D::K + k] : 0.f;
+  // decoder weight -> LDS (backward) or this wave's fragment -> registers (forward), bias ->
+  // LDS (zero padded), X padding zeroed, once per workgroup
+  constexpr int NTF = WF ? D::NT : 1, WQ = WF ? D::KP / 4 : 1;
+  const int ntw = W % NTF;                       // the forward GEMM's output-column tile of this wave
+  float wq[WQ];
+  if constexpr (WF) {
+    const int o = ntw * 16 + t16;
+#pragma unroll
+    for (int kq = 0; kq < WQ; ++kq) {
+      const int k = 4 * kq + g;
+      wq[kq] = (o < D::R && k < D::K) ? A.W[o * D::K + k] : 0.f;
+    }
+  } else {
+    #pragma unroll 1
+    for (int i = tid; i < D::NP * D::XS; i += LTHREADS) {
+      const int o = i / D::XS, k = i - o * D::XS;
+      Wl[i] = (o < D::R && k < D::K) ? A.W[o * D::K + k] : 0.f;
+    }
   }
   #pragma unroll 1
   for (int i = tid; i < SP * D::XS; i += LTHREADS) X[i] = 0.f;
@@ -147,7 +166,8 @@ __device__ void loss_body(const LArgs& A, float* lds) {
     }
     // per-region inputs of this group, loaded before the next group's prefetch
     float yv = -1.f, mu_in = 0.f, sd_in = 1.f;
-    const int rq = tid >> 2, part = tid & 3;     // 4 lanes per region
+    constexpr int LPR = D::LPR;
+    const int rq = tid / LPR, part = tid % LPR;  // LPR lanes per region
     if (rq < D::R) {
       yv = A.y[((size_t)b * A.T + t) * D::R + rq];
       if (BWD) {
@@ -160,33 +180,85 @@ __device__ void loss_body(const LArgs& A, float* lds) {
     }
     lds_barrier();
     // ---- P = X W^T + b  (S x R), one (M, N) tile per wave step ----------------------
-    for (int id = W; id < (SP / 16) * D::NT; id += LWAVES) {
-      const int mt = id / D::NT, nt = id - mt * D::NT;
-      f4 acc = f4zero();
-#pragma unroll 8
-      for (int kq = 0; kq < D::KP / 4; ++kq)
-        acc = mfma4(X[(mt * 16 + t16) * D::XS + 4 * kq + g], Wl[(nt * 16 + t16) * D::XS + 4 * kq + g], acc);
-      const float bv = bl[nt * 16 + t16];
+    if constexpr (WF) {
+      // this wave's tiles all have column tile ntw: two at a time (independent MFMA chains),
+      // B operand from registers, A operands read in batches ahead of their MFMAs
+      const int ntl = (SP / 16) * D::NT;
+      const float bv = bl[ntw * 16 + t16];
+      for (int id = W; id < ntl; id += 2 * LWAVES) {
+        const int mt0 = id / D::NT, id1 = id + LWAVES;
+        const bool two = id1 < ntl;
+        const int mt1 = two ? id1 / D::NT : mt0;
+        const float* x0 = X + (mt0 * 16 + t16) * D::XS + g;
+        const float* x1 = X + (mt1 * 16 + t16) * D::XS + g;
+        f4 acc0 = f4zero(), acc1 = f4zero();
+        constexpr int QB = 8;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) P[(mt * 16 + 4 * g + e) * D::PS + nt * 16 + t16] = acc[e] + bv;
+        for (int q0 = 0; q0 < WQ; q0 += QB) {
+          float a0[QB], a1[QB];
+#pragma unroll
+          for (int q = 0; q < QB; ++q)
+            if (q0 + q < WQ) { a0[q] = x0[4 * (q0 + q)]; a1[q] = x1[4 * (q0 + q)]; }
+#pragma unroll
+          for (int q = 0; q < QB; ++q)
+            if (q0 + q < WQ) {
+              acc0 = mfma4(a0[q], wq[q0 + q], acc0);
+              acc1 = mfma4(a1[q], wq[q0 + q], acc1);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) P[(mt0 * 16 + 4 * g + e) * D::PS + ntw * 16 + t16] = acc0[e] + bv;
+        if (two) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) P[(mt1 * 16 + 4 * g + e) * D::PS + ntw * 16 + t16] = acc1[e] + bv;
+        }
+      }
+    } else {
+      for (int id = W; id < (SP / 16) * D::NT; id += LWAVES) {
+        const int mt = id / D::NT, nt = id - mt * D::NT;
+        f4 acc = f4zero();
+#pragma unroll 8
+        for (int kq = 0; kq < D::KP / 4; ++kq)
+          acc = mfma4(X[(mt * 16 + t16) * D::XS + 4 * kq + g], Wl[(nt * 16 + t16) * D::XS + 4 * kq + g], acc);
+        const float bv = bl[nt * 16 + t16];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) P[(mt * 16 + 4 * g + e) * D::PS + nt * 16 + t16] = acc[e] + bv;
+      }
     }
     lds_barrier();
     // ---- per region (4 lanes each): mean / unbiased std over the samples; nll or
     //      d nll / d pred (in place of P) and its column sum (db) ---------------------
-    for (int r = rq; r < D::NP; r += LTHREADS / 4) {
+    for (int r = rq; r < D::NP; r += LTHREADS / LPR) {
       const bool real = r < D::R;
       float mu = mu_in, sd = sd_in;
       if (!BWD) {
-        float s1 = 0.f;
-        for (int s = part; s < S; s += 4) s1 += P[s * D::PS + r];
+        // the lane's samples s = part + LPR j read at once (one LDS latency), then two passes
+        constexpr int NV = SP_MAX / LPR;
+        float v[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const int s = part + LPR * j;
+          v[j] = s < S ? P[s * D::PS + r] : 0.f;
+        }
+        // fp64 sums: the mean is (nearly) correctly rounded, so the cancellation in the
+        // backward's sum_s (pred_s - mean) (the decoder-bias gradient) stays at rounding level
+        double s1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) s1 += (double)v[j];
         s1 += __shfl_xor(s1, 1, 64);
         s1 += __shfl_xor(s1, 2, 64);
-        mu = s1 / (float)S;
-        float s2 = 0.f;
-        for (int s = part; s < S; s += 4) { const float d = P[s * D::PS + r] - mu; s2 += d * d; }
+        s1 += __shfl_xor(s1, 4, 64);
+        mu = (float)(s1 / (double)S);
+        double s2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const float d = v[j] - mu;
+          s2 += part + LPR * j < S ? (double)(d * d) : 0.0;
+        }
         s2 += __shfl_xor(s2, 1, 64);
         s2 += __shfl_xor(s2, 2, 64);
-        sd = sqrtf(s2 / (float)(S - 1));
+        s2 += __shfl_xor(s2, 4, 64);
+        sd = sqrtf((float)(s2 / (double)(S - 1)));
         if (real && part == 0) {
           A.musd[(((size_t)t * A.B + b) * D::R + r) * 2] = mu;
           A.musd[(((size_t)t * A.B + b) * D::R + r) * 2 + 1] = sd;
@@ -206,15 +278,16 @@ __device__ void loss_body(const LArgs& A, float* lds) {
           cm = sc * dmu / (float)S;
           cs = sc * dsd * iv / (float)(S - 1);
         }
-        float s1 = 0.f;
-        for (int s = part; s < SP; s += 4) {
+        double s1 = 0.0;
+        for (int s = part; s < SP; s += LPR) {
           const float q = s < S ? cm + cs * (P[s * D::PS + r] - mu) : 0.f;
           P[s * D::PS + r] = q;
-          s1 += q;
+          s1 += (double)q;
         }
         s1 += __shfl_xor(s1, 1, 64);
         s1 += __shfl_xor(s1, 2, 64);
-        if (part == 0) bl[D::NP + r] += s1;     // aux row: db partial
+        s1 += __shfl_xor(s1, 4, 64);
+        if (part == 0) bl[D::NP + r] += (float)s1;     // aux row: db partial
       }
     }
     if constexpr (BWD) {

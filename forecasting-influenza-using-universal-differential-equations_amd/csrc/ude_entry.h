@@ -103,8 +103,8 @@ struct Ops {
     // BAYES: [eval][PACK_TOTAL] weight samples, then [eval][SLAB_TOTAL] eps in slab order
     o->pack_bytes = M::BAYES ? ne * (int64_t)(M::PACK_TOTAL + M::SLAB_TOTAL) * 4 : (int64_t)M::PACK_TOTAL * 4;
     o->sched_bytes = sched_bytes(p);
-    // stage inputs [tile][step][stage][F][16] (+ STORE_ACT: activations [tile][step][stage][16][ACT_A4])
-    o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * (M::F * TT + (M::STORE_ACT ? TT * M::ACT_A4 : 0)) * 4;
+    // stage inputs [tile][step][stage][F][16] (+ STORE_ACT / STORE_ACT_D: activations [tile][step][stage][16][ACT_A4])
+    o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::ACT_A4 : 0)) * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
     o->grad_slab_bytes = (int64_t)gb * M::SLAB_STRIDE * 4 + static_ws_floats(n_tiles) * 4;
     o->n_params = M::N_GRAD;

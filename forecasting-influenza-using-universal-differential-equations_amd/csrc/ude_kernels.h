@@ -232,7 +232,7 @@ struct NoWRegs {
   static constexpr bool ON = false;
   f4 wf[1], wb[1], wx[1];
 };
-template <class M, int W, bool BWD, bool NEED_F_ = !BWD || !M::STORE_ACT>
+template <class M, int W, bool BWD, bool NEED_F_ = !BWD || !M::ACT_STORED>
 struct WRegs {
   static constexpr bool ON = M::WREG;
   static constexpr bool NEED_F = NEED_F_;   // a stored-activation RK4 backward never runs the forward
@@ -467,17 +467,22 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
         mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
-        if constexpr (TRAIN && M::STORE_ACT) {
+        if constexpr (TRAIN && M::ACT_STORED) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
-          constexpr int QR = M::ACT_A4 / 4;
-          #pragma unroll
-          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
-            const int i = tid + u * NTHREADS;
-            if (i < TT * QR) {
-              const int t = i / QR, q = i - t * QR;
-              dst[i] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+          constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
+          // in chunks of UC quads (the forward runs two workgroups per CU: 256 registers)
+          constexpr int UC = NQ <= 5 ? NQ : 3;
+          #pragma unroll 1
+          for (int u0 = 0; u0 < NQ; u0 += UC) {
+#pragma unroll
+            for (int uu = 0; uu < UC; ++uu) {
+              const int i = tid + (u0 + uu) * NTHREADS;
+              if (u0 + uu < NQ && i < TT * QR) {
+                const int t = i / QR, q = i - t * QR;
+                dst[i] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+              }
             }
           }
         }
@@ -1185,7 +1190,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       });
     }
     __syncthreads();
-    if constexpr (!M::STORE_ACT) static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
+    if constexpr (!M::ACT_STORED) static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     __syncthreads();
@@ -1226,6 +1231,26 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         // stage input: from the staging slot the previous stage's flux pass filled,
         // or (first stage of the tile) straight from the forward's checkpoint
+        if constexpr (M::STORE_ACT_D) {
+          // this stage's activation rows straight from the forward's store (issued first: the
+          // stage-input copy below runs under their latency)
+          constexpr int QR = M::ACT_A4 / 4;
+          const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj));
+          f4 av[act_q_per_thread<M>()];
+#pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * QR) av[u] = src[i];
+          }
+#pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * QR) {
+              const int t = i / QR, q = i - t * QR;
+              *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = av[u];
+            }
+          }
+        }
         if (CARRY && have_next) {
           constexpr int QR = M::ACT_A4 / 4;
 #pragma unroll
@@ -1329,6 +1354,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           ckpt_issue<M>(A, tile, nstep, njj, ckn);
         }
         if constexpr (CARRY) {
+        } else if constexpr (M::STORE_ACT_D) {
+          if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+          flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         } else if constexpr (M::STORE_ACT) {
           // the stage's activations are the forward's (staged above); the next stage's are
           // fetched now and land in ACT_STG after the flux pass
@@ -1363,7 +1391,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
         if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        if constexpr (!M::STORE_ACT) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (next_out) {
           out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);

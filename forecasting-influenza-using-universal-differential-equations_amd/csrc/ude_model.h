@@ -156,6 +156,13 @@ struct Model {
   static constexpr int ACT_A = ACT_END - ACT0;
   static constexpr int ACT_A4 = (ACT_A + 3) & ~3;
   static constexpr bool STORE_ACT = SLOTS_ == 1 && !BAYES && ACT_A4 <= 512;
+  // Large records (R = 49: 162 KB of LDS, ~500 VGPRs in use) have no room to stage the next
+  // stage's rows, so the backward loads each stage's rows straight into the record at the stage
+  // start (STORE_ACT_D): one exposed HBM latency per stage instead of the recompute's four
+  // barrier-separated layer phases (a third of the backward's MFMA work).  1.5 GB for the
+  // 20,480-trajectory x 8-step state49 solve.
+  static constexpr bool STORE_ACT_D = !STORE_ACT && !BAYES;
+  static constexpr bool ACT_STORED = STORE_ACT || STORE_ACT_D;
   static constexpr int ACT_STG = X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0);
   static constexpr int LDS_B = (ACT_STG + (STORE_ACT ? TT * ACT_A4 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");

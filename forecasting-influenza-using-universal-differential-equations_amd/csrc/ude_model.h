@@ -155,7 +155,7 @@ struct Model {
   // 7.7 GB for the 4096 x 365-step north-star solve.
   static constexpr int ACT_A = ACT_END - ACT0;
   static constexpr int ACT_A4 = (ACT_A + 3) & ~3;
-  static constexpr bool STORE_ACT = SLOTS_ == 1 && !BAYES && ACT_A4 <= 512;
+  static constexpr bool STORE_ACT = SLOTS_ == 1 && ACT_A4 <= 512;
   // Large records (R = 49: 162 KB of LDS, ~500 VGPRs in use) have no room to stage the next
   // stage's rows, so the backward loads each stage's rows straight into the record at the stage
   // start (STORE_ACT_D): one exposed HBM latency per stage instead of the recompute's four

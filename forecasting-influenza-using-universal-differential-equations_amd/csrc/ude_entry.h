@@ -41,12 +41,12 @@ struct Ops {
   }
   // bytes of schedule copied into LDS behind a record of rec bytes: all of it when that does
   // not lower the kernel's occupancy, else 0 (read from global memory)
-  static int sched_lds(const void* kern, int rec, const UdeProblem* p) {
+  static int sched_lds(const void* kern, int rec, const UdeProblem* p, int threads = NTHREADS) {
     const int64_t sb = (sched_bytes(p) + 15) & ~(int64_t)15;
     if (sb == 0 || rec + sb > LDS_MAX) return 0;
     int o0 = 0, o1 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, kern, NTHREADS, rec) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, kern, NTHREADS, (size_t)(rec + sb)) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, kern, threads, rec) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, kern, threads, (size_t)(rec + sb)) != hipSuccess) return 0;
     return o1 >= o0 ? (int)sb : 0;
   }
   static_assert(!M::HOIST || DY0_STATIC_LDS <= 160 * 1024, "dy0 static time sums do not fit the 160 KiB LDS");
@@ -72,7 +72,7 @@ struct Ops {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     int of = 0, ob = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, (const void*)&ude_fwd_kernel<M, true>, NTHREADS, M::LDS_F));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_bwd_kernel<M>, NTHREADS, M::LDS_B));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_bwd_kernel<M>, M::BWD_THREADS, M::LDS_B));
     if (of < 1) of = 1;
     if (ob < 1) ob = 1;
     const long mf = (long)cus * of, mb = (long)cus * ob;
@@ -222,8 +222,8 @@ struct Ops {
 #endif
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
-    a.sched_lds = sched_lds((const void*)&ude_bwd_kernel<M>, M::LDS_B, p);
-    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B + a.sched_lds, s, a);
+    a.sched_lds = sched_lds((const void*)&ude_bwd_kernel<M>, M::LDS_B, p, M::BWD_THREADS);
+    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B + a.sched_lds, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);

@@ -644,7 +644,9 @@ struct RkAdjointEp {
 // BAYES: `es` addresses this evaluation's eps in slab order; every tile's dW
 // contribution of the evaluation is also accumulated eps-weighted into `dws` (and the
 // bias row sums into DBS): d|std| = sum_eval eps_eval * dW_eval (models_bayes.py:45-46).
-template <class M, int W, int SR, class DW, class DS, class G0, class EP0, class WR>
+// DX_ONLY (SPLIT_BWD critical-path waves): only the input gradients; the weight gradients of
+// the phase are the partner waves' (mlp_backward_dw).
+template <class M, int W, int SR, bool DX_ONLY = false, class DW, class DS, class G0, class EP0, class WR>
 __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
                                              Prof* pf, const EP0& ep0, const WR& wr) {
   constexpr bool RW = WR::ON;
@@ -682,7 +684,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
     // (one LDS latency per phase instead of one per tile).
     constexpr int NOWN = M::own_phase(W, d);
     constexpr int NDP = M::ndw_phase(W, d);
-    constexpr bool BATCH = !M::BAYES && NOWN > 0 && 4 * NOWN * 2 + 4 * NDP <= 96;
+    constexpr bool BATCH = !DX_ONLY && !M::BAYES && NOWN > 0 && 4 * NOWN * 2 + 4 * NDP <= 96;
     if constexpr (BATCH) {
       f4 gvv[NOWN];
       float gaa[NOWN][4], bva[NDP][4];
@@ -735,7 +737,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         }
       });
       __builtin_amdgcn_sched_barrier(0);
-    } else
+    } else if constexpr (!DX_ONLY)
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
@@ -891,6 +893,46 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
     });
     __syncthreads();
     UDE_STAMP(pf, 7 + d);
+  });
+}
+
+// Weight gradients of one backward stage on the SPLIT_BWD partner waves (W = the index of the
+// critical-path wave sharing the SIMD): the same barrier sequence as mlp_backward, and in phase
+// d the rows the wave owns: dW += g . in^T (MFMA, K = the tile's 16 trajectories) from the
+// phase's LDS operands, and per-trajectory bias sums in registers (reduced over the trajectories
+// once, at the launch end, instead of a cross-lane reduction every phase).
+template <class M, int W, int SR>
+__device__ __forceinline__ void mlp_backward_dw(const float* lds, f4* dw, f4* g0t, f4* gacc, int lane) {
+  const int t = lane & 15, g = lane >> 4;
+  const float* rec = lds + t * SR;
+  sfor<M::D>([&](auto ee) {
+    constexpr int d = M::D - 1 - decltype(ee)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k), rt = M::frt(d, k), goff = M::gbuf(net, d);
+        constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
+        constexpr int NC = M::rti(net, d);
+        const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
+        float ga[4], bv[4][NC];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
+#pragma unroll
+          for (int ct = 0; ct < NC; ++ct) bv[s][ct] = lds[(4 * g + s) * SR + inoff + ct * 16 + t];
+        }
+        if constexpr (d == 0) g0t[M::nz_before(W, k)] += gv;
+        else gacc[M::ng_before(W, d, k)] += gv;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          sfor<NC>([&](auto cc) {
+            constexpr int ct = decltype(cc)::value;
+            constexpr int idx = M::ndw_before(W, d, k) + ct;
+            dw[idx] = mfma4(ga[s], bv[s][ct], dw[idx]);
+          });
+      }
+    });
+    __syncthreads();
   });
 }
 
@@ -1096,6 +1138,55 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
   }
 }
 
+// Tile end (deterministic RHS): per-trajectory layer-0 gradient sums -> global (the
+// static-feature gradients are computed from them by ude_static_*_kernel); their trajectory
+// sums -> the workgroup's bias row sums in LDS.
+template <class M, int W>
+__device__ __forceinline__ void g0_tile_end(const KArgs& A, float* lds, const f4* g0t, int tile, int lane) {
+  const int t16 = lane & 15, g = lane >> 4;
+  sfor<M::FT(0)>([&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    if constexpr (M::fowner(0, k) == W) {
+      const f4 gv = g0t[M::nz_before(W, k)];
+      if constexpr (M::HOIST) {
+        float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
+        dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
+      }
+      f4 r = gv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+        r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+      }
+      if (t16 == 0) {
+        float* db = lds + M::DB_LDS + k * 16 + g * 4;
+        db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+      }
+    }
+  });
+}
+
+// Kernel end: wave W's dW register tiles (and BAYES eps-weighted ones) -> the workgroup slab.
+template <class M, int W, class DW, class DS>
+__device__ __forceinline__ void dw_to_slab(const DW& dw, const DS& dws, float* myslab, int lane) {
+  sfor<M::D>([&](auto dd) {
+    constexpr int d = decltype(dd)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k);
+        sfor<M::rti(net, d)>([&](auto cc) {
+          constexpr int ct = decltype(cc)::value;
+          reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
+          if constexpr (M::BAYES)
+            reinterpret_cast<f4*>(myslab + M::SLAB_TOTAL + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] =
+                dws[M::ndw_before(W, d, k) + ct];
+        });
+      }
+    });
+  });
+}
+
 template <class M, int W>
 __device__ void bwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_B;
@@ -1128,9 +1219,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
   }
 
-  f4 dw[NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
+  // SPLIT_BWD: the weight-gradient accumulators live on the partner waves (bwd_wbody)
+  f4 dw[M::SPLIT_BWD ? 1 : NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
 #pragma unroll
-  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  for (int i = 0; i < (M::SPLIT_BWD ? 1 : NDWn); ++i) dw[i] = f4zero();
   if constexpr (M::BAYES) {
 #pragma unroll
     for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
@@ -1426,7 +1518,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);
-        mlp_backward<M, W, SR>(rse, es, lds, dw, dws, g0t, lane, pf, RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
+        mlp_backward<M, W, SR, M::SPLIT_BWD>(rse, es, lds, dw, dws, g0t, lane, pf,
+                                             RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
         if constexpr (M::SPLITX0) {
           // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
           // use the step-end thread <-> (t, quad) mapping, so the step end needs no barrier.
@@ -1508,46 +1601,14 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     // per-trajectory layer-0 gradient sums -> global (static-feature gradients are
     // computed from them by ude_static_*_kernel); their trajectory sums -> bias row sums
     // (BAYES: layer-0 bias and static columns were accumulated per evaluation instead)
-    if constexpr (!M::BAYES) sfor<M::FT(0)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(0, k) == W) {
-        const f4 gv = g0t[M::nz_before(W, k)];
-        if constexpr (M::HOIST) {
-          float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
-          dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
-        }
-        f4 r = gv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-        }
-        if (t16 == 0) {
-          float* db = lds + M::DB_LDS + k * 16 + g * 4;
-          db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
-        }
-      }
-    });
+    if constexpr (!M::BAYES && !M::SPLIT_BWD) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
     __syncthreads();
   }
 
   // ---- kernel end: register tiles + LDS row sums -> this workgroup's slab ----
-  sfor<M::D>([&](auto dd) {
-    constexpr int d = decltype(dd)::value;
-    sfor<M::FT(d)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(d, k) == W) {
-        constexpr int net = M::fnet(d, k);
-        sfor<M::rti(net, d)>([&](auto cc) {
-          constexpr int ct = decltype(cc)::value;
-          reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
-          if constexpr (M::BAYES)
-            reinterpret_cast<f4*>(myslab + M::SLAB_TOTAL + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] =
-                dws[M::ndw_before(W, d, k) + ct];
-        });
-      }
-    });
-  });
+  if constexpr (!M::SPLIT_BWD) dw_to_slab<M, W>(dw, dws, myslab, lane);
+  // SPLIT_BWD: the partner waves' last bias row sums land before this barrier
+  if constexpr (M::SPLIT_BWD) __syncthreads();
   #pragma unroll 1
   for (int i = tid; i < M::NDB; i += NTHREADS) {
     myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
@@ -1557,11 +1618,79 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
 #endif
 }
+// SPLIT_BWD partner wave W + 4: the weight gradients of every stage (mlp_backward_dw), on the
+// exact barrier sequence of bwd_body's critical-path waves (every __syncthreads there has its
+// counterpart here, in the same order).
+template <class M, int W>
+__device__ void bwd_wbody(const KArgs& A, float* lds) {
+  constexpr int SR = M::SR_B;
+  constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
+  constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  constexpr int NGn = M::NG(W) > 0 ? M::NG(W) : 1;
+  const int lane = threadIdx.x & 63, t16 = lane & 15, g = lane >> 4;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
+  f4 dw[NDWn], g0t[NZn], gacc[NGn];
+#pragma unroll
+  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+#pragma unroll
+  for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
+  if (A.sched_lds > 0) __syncthreads();       // stage_sched: schedule copied into LDS
+  __syncthreads();                            // record zeroed
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    __syncthreads();                          // last step's output cotangents staged
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    __syncthreads();
+    for (int step = A.n_steps - 1; step >= 0; --step) {
+      #pragma unroll 1
+      for (int jj = 3; jj >= 0; --jj) {
+        __syncthreads();                      // stage input + activation rows in the record
+        __syncthreads();                      // flux pass: final-layer gradients written
+        mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);
+      }
+    }
+    __syncthreads();                          // tile end: dy0
+    __syncthreads();
+    g0_tile_end<M, W>(A, lds, g0t, tile, lane);
+    __syncthreads();
+  }
+  // kernel end: dW tiles -> slab; bias row sums of layers >= 1 from the per-trajectory sums
+  f4 none[1];
+  dw_to_slab<M, W>(dw, none, myslab, lane);
+  sfor<M::D>([&](auto dd) {
+    constexpr int d = decltype(dd)::value;
+    if constexpr (d > 0) sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        f4 r = gacc[M::ng_before(W, d, k)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+        }
+        if (t16 == 0) {
+          float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
+          db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+        }
+      }
+    });
+  });
+  __syncthreads();                            // bias row sums complete -> bwd_body copies them
+}
 
 template <class M>
-__global__ __launch_bounds__(NTHREADS) void ude_bwd_kernel(KArgs a) {
+__global__ __launch_bounds__(M::BWD_THREADS) void ude_bwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (M::SPLIT_BWD) {
+    if (w >= WAVES) {
+      if (w == 4) bwd_wbody<M, 0>(a, lds);
+      else if (w == 5) bwd_wbody<M, 1>(a, lds);
+      else if (w == 6) bwd_wbody<M, 2>(a, lds);
+      else bwd_wbody<M, 3>(a, lds);
+      return;
+    }
+  }
   if (w == 0) bwd_body<M, 0>(a, lds);
   else if (w == 1) bwd_body<M, 1>(a, lds);
   else if (w == 2) bwd_body<M, 2>(a, lds);

@@ -163,6 +163,14 @@ struct Model {
   // 20,480-trajectory x 8-step state49 solve.
   static constexpr bool STORE_ACT_D = !STORE_ACT && !BAYES;
   static constexpr bool ACT_STORED = STORE_ACT || STORE_ACT_D;
+  // Two waves per SIMD in the backward of small deterministic records (SPLIT_BWD): at one tile
+  // per CU a single wave per SIMD leaves every LDS latency, epilogue and barrier of a stage's
+  // critical path (flux -> input gradients layer by layer -> RK adjoint) exposed.  Waves 0-3
+  // run that path; waves 4-7 accumulate the weight gradients of the same phase (which nothing
+  // in the stage waits for) from the same LDS operands, on the same SIMDs, so their MFMAs fill
+  // the critical path's gaps.
+  static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !BAYES;
+  static constexpr int BWD_THREADS = SPLIT_BWD ? 2 * NTHREADS : NTHREADS;
   static constexpr int ACT_STG = X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0);
   static constexpr int LDS_B = (ACT_STG + (STORE_ACT ? TT * ACT_A4 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");

@@ -628,15 +628,23 @@ struct RkAdjointEp {
     f4* dk1 = reinterpret_cast<f4*>(rec + M::RK_DK1 + f0);
     f4* dk2 = reinterpret_cast<f4*>(rec + M::RK_DK2 + f0);
     f4* dk3 = reinterpret_cast<f4*>(rec + M::RK_DK3 + f0);
-    *accy += dY;
+    // every read before the first write: one LDS round trip, not one per accumulator
+    const f4 a = *accy, k1 = *dk1, k2 = *dk2, k3 = *dk3;
+    rk_adjoint_update(dY, dt, jj, a, k1, k2, k3, accy, dk1, dk2, dk3);
+  }
+  // 3/8-rule stage-input adjoint: accy += dY and the stage cotangents of the stages before jj
+  //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
+  static __device__ __forceinline__ void rk_adjoint_update(f4 dY, float dt, int jj, f4 a, f4 k1, f4 k2, f4 k3,
+                                                           f4* accy, f4* dk1, f4* dk2, f4* dk3) {
+    *accy = a + dY;
     if (jj == 3) {
       const f4 u = dt * dY;
-      *dk1 += u; *dk2 -= u; *dk3 += u;
+      *dk1 = k1 + u; *dk2 = k2 - u; *dk3 = k3 + u;
     } else if (jj == 2) {
       const f4 u = dt * dY;
-      *dk2 += u; *dk1 -= u * (1.0f / 3.0f);
+      *dk2 = k2 + u; *dk1 = k1 - u * (1.0f / 3.0f);
     } else if (jj == 1) {
-      *dk1 += (dY * (1.0f / 3.0f)) * dt;
+      *dk1 = k1 + (dY * (1.0f / 3.0f)) * dt;
     }
   }
 };
@@ -815,22 +823,30 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       // partial input gradient of every layer-0 tile over this wave's K quads, to LDS;
       // summed (fixed wave order) and fed to the RK adjoint by bwd_body after the barrier
       constexpr int PQ = M::HAS_P ? M::kout(0, 0) / 16 : 0;
-      sfor<M::XT(0)>([&](auto mm) { xa[decltype(mm)::value] = f4zero(); });
+      // two accumulation chains per tile (even / odd K steps): half the dependent-MFMA latency
+      f4 xo[M::XT(0)];
+      sfor<M::XT(0)>([&](auto mm) { xa[decltype(mm)::value] = f4zero(); xo[decltype(mm)::value] = f4zero(); });
+      f4 xq[M::x0q_w(W) > 0 ? M::x0q_w(W) : 1];
       sfor<M::x0q_w(W)>([&](auto jj) {
         constexpr int j = decltype(jj)::value, qq = W + j * WAVES;
         constexpr int net = qq < PQ ? 0 : 1, q = qq < PQ ? qq : qq - PQ;
         constexpr int KP = M::kout(net, 0);
-        const f4 x = *reinterpret_cast<const f4*>(rec + M::gbuf(net, 0) + g * (KP / 4) + 4 * q);
+        xq[j] = *reinterpret_cast<const f4*>(rec + M::gbuf(net, 0) + g * (KP / 4) + 4 * q);
+      });
+      sfor<M::x0q_w(W)>([&](auto jj) {
+        constexpr int j = decltype(jj)::value;
+        const f4 x = xq[j];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; e += 2)
           sfor<M::XT(0)>([&](auto mm) {
             constexpr int m = decltype(mm)::value;
             xa[m] = mfma4(FX(m * M::x0q_w(W) + j)[e], x[e], xa[m]);
+            xo[m] = mfma4(FX(m * M::x0q_w(W) + j)[e + 1], x[e + 1], xo[m]);
           });
       });
       sfor<M::XT(0)>([&](auto mm) {
         constexpr int m = decltype(mm)::value;
-        *reinterpret_cast<f4*>(lds + M::X0P_LDS + ((W * M::XT(0) + m) * 64 + lane) * 4) = xa[m];
+        *reinterpret_cast<f4*>(lds + M::X0P_LDS + ((W * M::XT(0) + m) * 64 + lane) * 4) = xa[m] + xo[m];
       });
       __syncthreads();
       UDE_STAMP(pf, 7 + d);
@@ -1033,6 +1049,35 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
 #pragma unroll
       for (int e = 0; e < 4; ++e) { Y[4 * v + e] = y[e]; dk[4 * v + e] = k[e]; }
     }
+    // the RK adjoint accumulators this stage updates, read with the other operands (every LDS
+    // read of the item before its first write: one round trip)
+    f4 ra[3], r1[3], r2[3], r3[3];
+    if constexpr (M::HAS_P) {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        ra[v] = *reinterpret_cast<const f4*>(rec + M::RK_ACCY + f0 + 4 * v);
+        r1[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK1 + f0 + 4 * v);
+        r2[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK2 + f0 + 4 * v);
+        r3[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK3 + f0 + 4 * v);
+      }
+    }
+    float qv[8], fav[12];
+    if constexpr (M::HAS_P) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const f4 x = *reinterpret_cast<const f4*>(rec + QO + 8 * rg + 4 * v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qv[4 * v + e] = x[e];
+      }
+    }
+    if constexpr (M::HAS_A) {
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const f4 fa = *reinterpret_cast<const f4*>(rec + FO + f0 + 4 * v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) fav[4 * v + e] = fa[e];
+      }
+    }
     if (jj == 3) {
 #pragma unroll
       for (int i = 0; i < 12; ++i) dk[i] = (dk[i] * 0.125f) * dt;
@@ -1045,15 +1090,10 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     if constexpr (M::HAS_A) {
       float dfa[12];
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        const f4 fa = *reinterpret_cast<const f4*>(rec + FO + f0 + 4 * v);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * v + e;
-          const bool live = valid && (4 * rg + i / 3) < M::R;
-          const float d = M::HAS_P ? A.fa_w * dres[i] : dres[i];
-          dfa[i] = live ? d + cn * fa[e] : 0.f;
-        }
+      for (int i = 0; i < 12; ++i) {
+        const bool live = valid && (4 * rg + i / 3) < M::R;
+        const float d = M::HAS_P ? A.fa_w * dres[i] : dres[i];
+        dfa[i] = live ? d + cn * fav[i] : 0.f;
       }
       if constexpr (VEC_F) {
 #pragma unroll
@@ -1071,13 +1111,8 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
 #pragma unroll
     for (int i = 0; i < 12; ++i) dyf[i] = 0.f;
     if constexpr (M::HAS_P) {
-      float q[8], dq[8];
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const f4 x = *reinterpret_cast<const f4*>(rec + QO + 8 * rg + 4 * v);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) q[4 * v + e] = x[e];
-      }
+      const float* q = qv;
+      float dq[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool live = valid && (4 * rg + j) < M::R;
@@ -1118,7 +1153,12 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
 #pragma unroll
       for (int v = 0; v < 3; ++v) {
         const f4 dY = {dyf[4 * v], dyf[4 * v + 1], dyf[4 * v + 2], dyf[4 * v + 3]};
-        RkAdjointEp<M, SR>{rec, dt, jj}(f0 + 4 * v, dY);
+        const int f = f0 + 4 * v;
+        RkAdjointEp<M, SR>::rk_adjoint_update(dY, dt, jj, ra[v], r1[v], r2[v], r3[v],
+                                              reinterpret_cast<f4*>(rec + M::RK_ACCY + f),
+                                              reinterpret_cast<f4*>(rec + M::RK_DK1 + f),
+                                              reinterpret_cast<f4*>(rec + M::RK_DK2 + f),
+                                              reinterpret_cast<f4*>(rec + M::RK_DK3 + f));
       }
     }
     // the padded rows of the final-layer gradient slots (the slots alias wider layers'
@@ -1296,6 +1336,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     constexpr bool CARRY = M::STORE_ACT && SL == 1;
     f4 actr[CARRY ? act_q_per_thread<M>() : 1];
     float ckr[SL][3];
+    // CARRY: the next step's output cotangents are loaded at stage 1 of the step (a whole stage
+    // ahead of the flux pass of stage 0 that consumes them)
+    float gvc[SL][3];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's
@@ -1428,9 +1471,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         constexpr bool EARLY_CK = SL == 1;
         if constexpr (CARRY) {
-          // output cotangent loads first: out_finish below waits for them with the carried
-          // loads (issued after) still in flight
-          if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
+          // output cotangent loads first: out_finish waits for them with the carried loads
+          // (issued after) still in flight
+          if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvc);
           if (have_next) {
             ckpt_issue<M>(A, tile, nstep, njj, ckr);
             constexpr int QR = M::ACT_A4 / 4;
@@ -1486,7 +1529,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (next_out) {
-          out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
+          out_finish<M>(A, sc, nstep, n0, CARRY ? gvc : gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
           sfor<SL>([&](auto ss) {

@@ -69,6 +69,12 @@ struct KArgs {
                               // null (its dims >= 3 all zero); exactly one of the two is set
 };
 
+// Timing ablations for a diagnostic build (-DUDE_ABL=n, tools/ablate.py): component n of the
+// small-record backward is skipped (results are wrong; only the kernel time is read).
+#ifndef UDE_ABL
+#define UDE_ABL 0
+#endif
+
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
 constexpr int NPROF = 20;
@@ -884,7 +890,8 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
             sfor<M::XT(d)>([&](auto mm) {
               constexpr int m = decltype(mm)::value;
               if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net))
-                xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
+                if constexpr (UDE_ABL != 3) xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
+                else xa[m][e] += x[e];
             });
         }
       }
@@ -925,7 +932,7 @@ __device__ __forceinline__ void mlp_backward_dw(const float* lds, f4* dw, f4* g0
     constexpr int d = M::D - 1 - decltype(ee)::value;
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(d, k) == W) {
+      if constexpr (M::fowner(d, k) == W && !(UDE_ABL == 6 && d == 1)) {
         constexpr int net = M::fnet(d, k), rt = M::frt(d, k), goff = M::gbuf(net, d);
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
         constexpr int NC = M::rti(net, d);
@@ -1034,16 +1041,22 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
   constexpr int FO = M::HAS_A ? M::act_off(1, M::nl(1) - 1) : 0, FG = M::HAS_A ? M::gbuf(1, M::nl(1) - 1) : 0;
   constexpr bool VEC_Q = !M::HAS_P || M::QW <= M::kout(0, M::nl(0) - 1);
   constexpr bool VEC_F = !M::HAS_A || M::F4 <= M::kout(1, M::nl(1) - 1);
+  // G regions per item: 4 (12 features, 8 rates: 16-B LDS ops), or all of them when R < 4 (one
+  // item per trajectory with only its live features: at R = 1 a quarter of the VALU and LDS
+  // work of a 4-region group, on the single wave that runs the pass)
+  constexpr int G = M::R < 4 ? M::R : 4;
+  constexpr int NQF = (3 * G + 3) / 4, NQR = (2 * G + 3) / 4;   // feature / rate quads per item
+  constexpr int NF = 4 * NQF, NR = 4 * NQR;
   #pragma unroll 1
   for (int it = threadIdx.x; it < ITEMS; it += NTHREADS) {
     const int t = it & (TT - 1), rg = it >> 4;
     const bool valid = n0 + t < A.n_traj;
     float* rec = lds + t * SR;
-    float Y[12], dk[12], dres[12];
+    float Y[NF], dk[NF], dres[NF];
     const int f0 = 12 * rg;
     const int dko = jj == 3 ? M::RK_A : jj == 2 ? M::RK_DK3 : jj == 1 ? M::RK_DK2 : M::RK_DK1;
 #pragma unroll
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < NQF; ++v) {
       const f4 y = *reinterpret_cast<const f4*>(rec + M::Y_OFF + f0 + 4 * v);
       const f4 k = *reinterpret_cast<const f4*>(rec + dko + f0 + 4 * v);
 #pragma unroll
@@ -1051,20 +1064,20 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     }
     // the RK adjoint accumulators this stage updates, read with the other operands (every LDS
     // read of the item before its first write: one round trip)
-    f4 ra[3], r1[3], r2[3], r3[3];
+    f4 ra[NQF], r1[NQF], r2[NQF], r3[NQF];
     if constexpr (M::HAS_P) {
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
+      for (int v = 0; v < NQF; ++v) {
         ra[v] = *reinterpret_cast<const f4*>(rec + M::RK_ACCY + f0 + 4 * v);
         r1[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK1 + f0 + 4 * v);
         r2[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK2 + f0 + 4 * v);
         r3[v] = *reinterpret_cast<const f4*>(rec + M::RK_DK3 + f0 + 4 * v);
       }
     }
-    float qv[8], fav[12];
+    float qv[NR], fav[NF];
     if constexpr (M::HAS_P) {
 #pragma unroll
-      for (int v = 0; v < 2; ++v) {
+      for (int v = 0; v < NQR; ++v) {
         const f4 x = *reinterpret_cast<const f4*>(rec + QO + 8 * rg + 4 * v);
 #pragma unroll
         for (int e = 0; e < 4; ++e) qv[4 * v + e] = x[e];
@@ -1072,7 +1085,7 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     }
     if constexpr (M::HAS_A) {
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
+      for (int v = 0; v < NQF; ++v) {
         const f4 fa = *reinterpret_cast<const f4*>(rec + FO + f0 + 4 * v);
 #pragma unroll
         for (int e = 0; e < 4; ++e) fav[4 * v + e] = fa[e];
@@ -1080,41 +1093,43 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     }
     if (jj == 3) {
 #pragma unroll
-      for (int i = 0; i < 12; ++i) dk[i] = (dk[i] * 0.125f) * dt;
+      for (int i = 0; i < NF; ++i) dk[i] = (dk[i] * 0.125f) * dt;
     }
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const bool live = valid && (4 * rg + i / 3) < M::R;
+    for (int i = 0; i < NF; ++i) {
+      const bool live = valid && i < 3 * G && (4 * rg + i / 3) < M::R;
       dres[i] = (!live || Y[i] > 2.f || Y[i] < -1.f) ? 0.f : dk[i];
     }
     if constexpr (M::HAS_A) {
-      float dfa[12];
+      float dfa[NF];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const bool live = valid && (4 * rg + i / 3) < M::R;
+      for (int i = 0; i < NF; ++i) {
+        const bool live = valid && i < 3 * G && (4 * rg + i / 3) < M::R;
         const float d = M::HAS_P ? A.fa_w * dres[i] : dres[i];
         dfa[i] = live ? d + cn * fav[i] : 0.f;
       }
       if constexpr (VEC_F) {
 #pragma unroll
-        for (int v = 0; v < 3; ++v) {
+        for (int v = 0; v < NQF; ++v) {
           f4 o = {dfa[4 * v], dfa[4 * v + 1], dfa[4 * v + 2], dfa[4 * v + 3]};
           *reinterpret_cast<f4*>(rec + FG + f0 + 4 * v) = o;
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 12; ++i)
+        for (int i = 0; i < NF; ++i)
           if (f0 + i < M::kout(1, M::nl(1) - 1)) rec[FG + f0 + i] = dfa[i];
       }
     }
-    float dyf[12];
+    float dyf[NF];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) dyf[i] = 0.f;
+    for (int i = 0; i < NF; ++i) dyf[i] = 0.f;
     if constexpr (M::HAS_P) {
       const float* q = qv;
-      float dq[8];
+      float dq[NR];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int i = 0; i < NR; ++i) dq[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
         const bool live = valid && (4 * rg + j) < M::R;
         const float* y = Y + 3 * j;
         const float* dr = dres + 3 * j;
@@ -1138,20 +1153,20 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
       }
       if constexpr (VEC_Q) {
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < NQR; ++v) {
           f4 o = {dq[4 * v], dq[4 * v + 1], dq[4 * v + 2], dq[4 * v + 3]};
           *reinterpret_cast<f4*>(rec + QG + 8 * rg + 4 * v) = o;
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < NR; ++i)
           if (8 * rg + i < M::kout(0, M::nl(0) - 1)) rec[QG + 8 * rg + i] = dq[i];
       }
       // RK4 (3/8 rule) adjoint of the stage input, direct (flux) part; the MLP part
       // is added by mlp_backward's layer-0 epilogue (RkAdjointEp)
       //   Y2 = y + (dt k1)/3, Y3 = y + dt (k2 - k1/3), Y4 = y + dt (k1 - k2 + k3)
 #pragma unroll
-      for (int v = 0; v < 3; ++v) {
+      for (int v = 0; v < NQF; ++v) {
         const f4 dY = {dyf[4 * v], dyf[4 * v + 1], dyf[4 * v + 2], dyf[4 * v + 3]};
         const int f = f0 + 4 * v;
         RkAdjointEp<M, SR>::rk_adjoint_update(dY, dt, jj, ra[v], r1[v], r2[v], r3[v],
@@ -1165,12 +1180,12 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     // gradients, so they are re-zeroed every stage), by the item of the last region group
     if (rg == RG - 1) {
       if constexpr (M::HAS_P) {
-        constexpr int lo = cmin(M::QW, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
+        constexpr int lo = cmin(8 * (RG - 1) + 4 * NQR, M::kout(0, M::nl(0) - 1)), hi = M::kout(0, M::nl(0) - 1);
 #pragma unroll
         for (int o = lo; o < hi; o += 4) *reinterpret_cast<f4*>(rec + QG + o) = f4zero();
       }
       if constexpr (M::HAS_A) {
-        constexpr int lo = cmin(M::F4, M::kout(1, M::nl(1) - 1)), hi = M::kout(1, M::nl(1) - 1);
+        constexpr int lo = cmin(12 * (RG - 1) + 4 * NQF, M::kout(1, M::nl(1) - 1)), hi = M::kout(1, M::nl(1) - 1);
 #pragma unroll
         for (int o = lo; o < hi; o += 4) *reinterpret_cast<f4*>(rec + FG + o) = f4zero();
       }
@@ -1345,7 +1360,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       // output cotangents (y_n-side share staged in DK3); set up the accumulators and
       // the stage cotangents of the 3/8 combination dy = (k1 + 3 (k2 + k3) + k4) dt / 8.
       {
-        constexpr int NV = M::F4 / 4;
+        constexpr int NV = M::NVL;
         #pragma unroll 1
         for (int i = tid; i < TT * NV; i += NTHREADS) {
           const int t = i / NV, v = i - t * NV;
@@ -1386,7 +1401,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
             }
           }
         }
-        if (CARRY && have_next) {
+        if (CARRY && have_next && UDE_ABL != 4) {
           constexpr int QR = M::ACT_A4 / 4;
 #pragma unroll
           for (int u = 0; u < act_q_per_thread<M>(); ++u) {
@@ -1484,7 +1499,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
               if (i < TT * QR) actr[u] = src[i];
             }
           }
-          flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+          if constexpr (UDE_ABL != 2) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         } else if (EARLY_CK && have_next) {
           ckpt_issue<M>(A, tile, nstep, njj, ckn);
         }
@@ -1561,7 +1576,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         UDE_STAMP(pf, 6);
         __syncthreads();
         UDE_STAMP(pf, 11);
-        mlp_backward<M, W, SR, M::SPLIT_BWD>(rse, es, lds, dw, dws, g0t, lane, pf,
+        if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { __syncthreads(); });
+        else mlp_backward<M, W, SR, M::SPLIT_BWD>(rse, es, lds, dw, dws, g0t, lane, pf,
                                              RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
         if constexpr (M::SPLITX0) {
           // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
@@ -1574,11 +1590,11 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
               v += *reinterpret_cast<const f4*>(lds + M::X0P_LDS + ((w * M::XT(0) + m) * 64 + li) * 4);
             return v;
           };
-          constexpr int NV = M::F4 / 4, NVX = cmin(M::F4, M::F16) / 4;
+          constexpr int NV = M::NVL, NVX = cmin(M::F4, M::F16) / 4;
           #pragma unroll 1
           for (int i = tid; i < TT * NV; i += NTHREADS) {
             const int t = i / NV, v = i - t * NV;
-            if (v < NVX) RkAdjointEp<M, SR>{lds + t * SR, dt, jj}(4 * v, x0sum(t, 4 * v));
+            if (UDE_ABL != 5 && v < NVX) RkAdjointEp<M, SR>{lds + t * SR, dt, jj}(4 * v, x0sum(t, 4 * v));
           }
           if constexpr (M::FULL0) {
             constexpr int NS = M::S16 / 4;
@@ -1594,7 +1610,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       }
       // step end (same thread <-> element mapping as the step start: no barrier)
       {
-        constexpr int NV = M::F4 / 4;
+        constexpr int NV = M::NVL;
         #pragma unroll 1
         for (int i = tid; i < TT * NV; i += NTHREADS) {
           const int t = i / NV, v = i - t * NV;
@@ -1689,7 +1705,8 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         __syncthreads();                      // stage input + activation rows in the record
         __syncthreads();                      // flux pass: final-layer gradients written
-        mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);
+        if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { __syncthreads(); }); }
+        else mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);
       }
     }
     __syncthreads();                          // tile end: dy0

@@ -120,6 +120,9 @@ struct Model {
   static constexpr int F4 = 12 * ((R + 3) / 4);
   static constexpr int SLOTS_ = (R * TT + NTHREADS - 1) / NTHREADS;   // == SLOTS
   static constexpr int QW = 8 * ((R + 3) / 4);
+  // quads of the RK-state rows holding live features (3R of them; the rest stay zero): the
+  // per-(trajectory, quad) RK passes of the backward touch only these
+  static constexpr int NVL = (3 * R + 3) / 4;
   static constexpr int RK_A = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);  // adjoint of y_{n+1} (carried across steps)
   static constexpr int RK_PEND = RK_A + F4;       // y_n-side share of interpolated outputs
   static constexpr int RK_ACCY = RK_PEND + F4;    // adjoint of y_n being accumulated

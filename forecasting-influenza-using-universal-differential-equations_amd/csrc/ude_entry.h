@@ -39,16 +39,6 @@ struct Ops {
   static int64_t sched_bytes(const UdeProblem* p) {
     return (int64_t)p->n_steps * 4 + (int64_t)(p->n_steps + 1) * 4 + (int64_t)p->n_out * 12;
   }
-  // bytes of schedule copied into LDS behind a record of rec bytes: all of it when that does
-  // not lower the kernel's occupancy, else 0 (read from global memory)
-  static int sched_lds(const void* kern, int rec, const UdeProblem* p, int threads = NTHREADS) {
-    const int64_t sb = (sched_bytes(p) + 15) & ~(int64_t)15;
-    if (sb == 0 || rec + sb > LDS_MAX) return 0;
-    int o0 = 0, o1 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, kern, threads, rec) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, kern, threads, (size_t)(rec + sb)) != hipSuccess) return 0;
-    return o1 >= o0 ? (int)sb : 0;
-  }
   static_assert(!M::HOIST || DY0_STATIC_LDS <= 160 * 1024, "dy0 static time sums do not fit the 160 KiB LDS");
   static int ensure_attrs() {
     static bool done = false;
@@ -187,9 +177,8 @@ struct Ops {
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
     const void* kf = ckpt ? (const void*)&ude_fwd_kernel<M, true> : (const void*)&ude_fwd_kernel<M, false>;
-    a.sched_lds = sched_lds(kf, M::LDS_F, p);
-    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F + a.sched_lds, s, a);
-    else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F + a.sched_lds, s, a);
+    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
     hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
@@ -222,8 +211,7 @@ struct Ops {
 #endif
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
-    a.sched_lds = sched_lds((const void*)&ude_bwd_kernel<M>, M::LDS_B, p, M::BWD_THREADS);
-    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B + a.sched_lds, s, a);
+    hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);

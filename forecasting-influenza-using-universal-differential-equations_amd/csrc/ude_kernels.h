@@ -60,7 +60,6 @@ struct KArgs {
   float* dy0;
   float* slab;
   int n_traj, n_steps, n_out, n_tiles;
-  int sched_lds;              // > 0: copy the schedule (this many bytes) into LDS after the record
   float fa_w;
   unsigned long long* prof;   // diagnostic builds only (-DUDE_PROFILE): per-segment cycle sums
   float* g0buf;               // backward: per-trajectory layer-0 gradient sums [tile][K0][16]
@@ -97,31 +96,25 @@ struct Prof {
 #define UDE_STAMP(pf, seg) do { } while (0)
 #endif
 
-// The step / output schedule is read every stage (dt, the output CSR): the launch copies it
-// into LDS behind the record when there is room (A.sched_lds), so those reads are LDS
-// round trips instead of dependent global loads on the stage's critical path.
-__device__ __forceinline__ const unsigned char* stage_sched(const KArgs& A, float* lds, int rec_bytes) {
-  if (A.sched_lds <= 0) return A.sched;
-  unsigned int* dst = reinterpret_cast<unsigned int*>(reinterpret_cast<unsigned char*>(lds) + rec_bytes);
-  const unsigned int* src = reinterpret_cast<const unsigned int*>(A.sched);
-  #pragma unroll 1
-  for (int i = threadIdx.x; i < A.sched_lds / 4; i += NTHREADS) dst[i] = src[i];
-  __syncthreads();
-  return reinterpret_cast<const unsigned char*>(dst);
-}
-
+// The step / output schedule (dt, the output CSR) is read every stage.  It is wave-uniform and
+// read-only, so it is read through the constant address space: scalar loads (s_load, scalar
+// cache) that count only in lgkmcnt.  A generic pointer compiled to FLAT loads, which count in
+// vmcnt as well, so every schedule read waited for all of the wave's in-flight global stores
+// (the forward's checkpoint and activation rows) and prefetch loads.
+typedef const __attribute__((address_space(4))) float* SchedF;
+typedef const __attribute__((address_space(4))) int* SchedI;
 struct Sched {
-  const float* dt;
-  const int* out_start;
-  const int* out_j;
-  const int* out_mode;
-  const float* out_slope;
+  SchedF dt;
+  SchedI out_start;
+  SchedI out_j;
+  SchedI out_mode;
+  SchedF out_slope;
   __device__ Sched(const unsigned char* base, int n_steps, int n_out) {
-    dt = (const float*)base;
-    out_start = (const int*)(dt + n_steps);
+    dt = (SchedF)base;
+    out_start = (SchedI)(dt + n_steps);
     out_j = out_start + n_steps + 1;
     out_mode = out_j + n_out;
-    out_slope = (const float*)(out_mode + n_out);
+    out_slope = (SchedF)(out_mode + n_out);
   }
 };
 
@@ -337,7 +330,8 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
               sfor<M::FT(d)>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
                 if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net)
-                  acc[k] = mfma4(FR(M::fq_before(W, d, k) + q)[e], x[e], acc[k]);
+                  if constexpr (UDE_ABL != 13) acc[k] = mfma4(FR(M::fq_before(W, d, k) + q)[e], x[e], acc[k]);
+                  else acc[k][e] += x[e];
               });
           }
         }
@@ -423,7 +417,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
   const int tid = threadIdx.x, lane = tid & 63;
-  const Sched sc(stage_sched(A, lds, M::LDS_F), A.n_steps, A.n_out);
+  const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
   double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
@@ -460,6 +454,21 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         }
       }
     });
+    // static latent dims (zero derivative, carried unchanged: lib/models.py:144) of every output
+    // time, once per tile (not in the step loop, where each copy waited on a global load)
+    if constexpr (M::L > 3) {
+      #pragma unroll 1
+      for (int i = tid; i < A.n_out * M::PAIRS; i += NTHREADS) {
+        const int o = i / M::PAIRS, p = i - o * M::PAIRS;
+        const int r = p / TT, t = p - r * TT, n = n0 + t;
+        if (n < A.n_traj) {
+          const float* src = A.y0 + ((size_t)n * M::R + r) * M::L;
+          float* dst = A.latent + (size_t)sc.out_j[o] * NRL + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+          for (int c = 3; c < M::L; ++c) dst[c] = src[c];
+        }
+      }
+    }
     load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
     __syncthreads();
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
@@ -473,7 +482,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
         mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
-        if constexpr (TRAIN && M::ACT_STORED) {
+        if constexpr (TRAIN && M::ACT_STORED && UDE_ABL != 11) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
@@ -492,7 +501,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             }
           }
         }
-        sfor<SL>([&](auto ss) {
+        if constexpr (UDE_ABL != 12) sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
           if (p < M::PAIRS) {
@@ -560,8 +569,6 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
                     else v = yold[c] + slope * (ys[sl][c] - yold[c]);
                     dst[c] = v;
                   }
-                  const float* src = A.y0 + ((size_t)n * M::R + r) * M::L;
-                  for (int c = 3; c < M::L; ++c) dst[c] = src[c];
                 }
               }
             }
@@ -1250,7 +1257,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int t16 = lane & 15, g = lane >> 4;
-  const Sched sc(stage_sched(A, lds, M::LDS_B), A.n_steps, A.n_out);
+  const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
@@ -1381,7 +1388,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         // stage input: from the staging slot the previous stage's flux pass filled,
         // or (first stage of the tile) straight from the forward's checkpoint
-        if constexpr (M::STORE_ACT_D) {
+        if constexpr (M::STORE_ACT_D && UDE_ABL != 8) {
           // this stage's activation rows straight from the forward's store (issued first: the
           // stage-input copy below runs under their latency)
           constexpr int QR = M::ACT_A4 / 4;
@@ -1693,7 +1700,6 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
 #pragma unroll
   for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
-  if (A.sched_lds > 0) __syncthreads();       // stage_sched: schedule copied into LDS
   __syncthreads();                            // record zeroed
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     __syncthreads();                          // last step's output cotangents staged

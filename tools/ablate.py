@@ -21,6 +21,9 @@ from ude_amd import _native, fused, solvers  # noqa: E402
 import bench  # noqa: E402
 
 IDS = [int(a) for a in sys.argv[1:] if a.isdigit()] or [0, 1, 2, 3, 4, 5, 6, 7]
+# extra flags per variant id >= 100 (id - 100 = UDE_ABL): UDE_DEFER=1
+def flags(i):
+    return [f"-DUDE_ABL={i % 100}"] + (["-DUDE_DEFER=1"] if i >= 100 else [])
 WL = os.environ.get("ABL_WORKLOAD", "us_northstar")
 
 
@@ -34,7 +37,7 @@ def main():
     if "--build" in sys.argv:
         with ThreadPoolExecutor(8) as ex:
             list(ex.map(lambda i: _native.build_library([cfg], lib_path(i), f"abl{i}_{WL}", jobs=1,
-                                                        extra_flags=[f"-DUDE_ABL={i}"]), IDS))
+                                                        extra_flags=flags(i)), IDS))
         print("built", IDS)
         return
     dev = torch.device("cuda", 0)

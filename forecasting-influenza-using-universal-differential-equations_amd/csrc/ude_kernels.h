@@ -47,6 +47,18 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 }
 __device__ __forceinline__ f4 f4zero() { f4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
+// Workgroup barrier for LDS hand-offs.  __syncthreads()'s workgroup-scope fence waits for every
+// outstanding memory operation of the wave (s_waitcnt vmcnt(0)), so each barrier of the stage
+// loop drained the prefetch loads issued a stage ahead (backward) and the checkpoint /
+// activation-row stores (forward), exposing their HBM latency at every phase.  The RK4 kernels
+// hand data between waves only through LDS (global results are read by later launches), so their
+// barriers fence the LDS address space only: in-flight global loads and stores cross them.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 struct KArgs {
   const float* pack;
   const float* y0;
@@ -349,7 +361,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
         *reinterpret_cast<f4*>(rec + M::act_off(net, d) + rt * 16 + g * 4) = a;
       }
     });
-    __syncthreads();
+    lds_sync();
     UDE_STAMP(pf, 2 + d);
   });
 }
@@ -427,7 +439,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 
   #pragma unroll 1
   for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
-  __syncthreads();
+  lds_sync();
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
@@ -470,10 +482,10 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
       }
     }
     load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
-    __syncthreads();
+    lds_sync();
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
     static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
-    __syncthreads();
+    lds_sync();
 
     for (int step = 0; step < A.n_steps; ++step) {
       const float dt = sc.dt[step];
@@ -585,7 +597,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             }
           }
         });
-        __syncthreads();
+        lds_sync();
       }
     }
   }
@@ -593,12 +605,12 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   // deterministic per-workgroup partial sums
   double* red = reinterpret_cast<double*>(lds);
   double v[5] = {wave_sum(st_b), wave_sum(st_g), wave_sum(st_bb), wave_sum(st_gg), wave_sum(st_fa)};
-  __syncthreads();
+  lds_sync();
   if (lane == 0) {
 #pragma unroll
     for (int c = 0; c < 5; ++c) red[(tid >> 6) * 5 + c] = v[c];
   }
-  __syncthreads();
+  lds_sync();
   if (tid < 5) {
     double s = 0;
     for (int w = 0; w < WAVES; ++w) s += red[w * 5 + tid];
@@ -861,7 +873,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         constexpr int m = decltype(mm)::value;
         *reinterpret_cast<f4*>(lds + M::X0P_LDS + ((W * M::XT(0) + m) * 64 + lane) * 4) = xa[m] + xo[m];
       });
-      __syncthreads();
+      lds_sync();
       UDE_STAMP(pf, 7 + d);
       return;
     }
@@ -921,7 +933,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         }
       }
     });
-    __syncthreads();
+    lds_sync();
     UDE_STAMP(pf, 7 + d);
   });
 }
@@ -962,7 +974,7 @@ __device__ __forceinline__ void mlp_backward_dw(const float* lds, f4* dw, f4* g0
           });
       }
     });
-    __syncthreads();
+    lds_sync();
   });
 }
 
@@ -1303,7 +1315,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 
   #pragma unroll 1
   for (int i = tid; i < M::LDS_B / 4; i += NTHREADS) lds[i] = 0.f;
-  __syncthreads();
+  lds_sync();
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
@@ -1343,11 +1355,11 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
       });
     }
-    __syncthreads();
+    lds_sync();
     if constexpr (!M::ACT_STORED) static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
-    __syncthreads();
+    lds_sync();
     UDE_STAMP(pf, 15);
 
     bool have_next = false;
@@ -1472,7 +1484,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 0);
-        __syncthreads();
+        lds_sync();
         UDE_STAMP(pf, 1);
         // at the step's last stage the next step's output cotangents are loaded from
         // fwd phase 1 on (consumed after the flux pass)
@@ -1581,9 +1593,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
         UDE_STAMP(pf, 18);
         UDE_STAMP(pf, 6);
-        __syncthreads();
+        lds_sync();
         UDE_STAMP(pf, 11);
-        if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { __syncthreads(); });
+        if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { lds_sync(); });
         else mlp_backward<M, W, SR, M::SPLIT_BWD>(rse, es, lds, dw, dws, g0t, lane, pf,
                                              RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
         if constexpr (M::SPLITX0) {
@@ -1630,7 +1642,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     }
 
     // ---- tile end: dy0 (dynamic), static-feature gradients, layer-0 bias sums ----
-    __syncthreads();
+    lds_sync();
     #pragma unroll 1
     for (int p = tid; p < M::PAIRS; p += NTHREADS) {
       const int r = p / TT, t = p - r * TT;
@@ -1663,18 +1675,18 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
       }
     }
-    __syncthreads();
+    lds_sync();
     // per-trajectory layer-0 gradient sums -> global (static-feature gradients are
     // computed from them by ude_static_*_kernel); their trajectory sums -> bias row sums
     // (BAYES: layer-0 bias and static columns were accumulated per evaluation instead)
     if constexpr (!M::BAYES && !M::SPLIT_BWD) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
-    __syncthreads();
+    lds_sync();
   }
 
   // ---- kernel end: register tiles + LDS row sums -> this workgroup's slab ----
   if constexpr (!M::SPLIT_BWD) dw_to_slab<M, W>(dw, dws, myslab, lane);
   // SPLIT_BWD: the partner waves' last bias row sums land before this barrier
-  if constexpr (M::SPLIT_BWD) __syncthreads();
+  if constexpr (M::SPLIT_BWD) lds_sync();
   #pragma unroll 1
   for (int i = tid; i < M::NDB; i += NTHREADS) {
     myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
@@ -1685,7 +1697,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 #endif
 }
 // SPLIT_BWD partner wave W + 4: the weight gradients of every stage (mlp_backward_dw), on the
-// exact barrier sequence of bwd_body's critical-path waves (every __syncthreads there has its
+// exact barrier sequence of bwd_body's critical-path waves (every lds_sync there has its
 // counterpart here, in the same order).
 template <class M, int W>
 __device__ void bwd_wbody(const KArgs& A, float* lds) {
@@ -1700,25 +1712,25 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
 #pragma unroll
   for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
-  __syncthreads();                            // record zeroed
+  lds_sync();                            // record zeroed
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
-    __syncthreads();                          // last step's output cotangents staged
+    lds_sync();                          // last step's output cotangents staged
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
-    __syncthreads();
+    lds_sync();
     for (int step = A.n_steps - 1; step >= 0; --step) {
       #pragma unroll 1
       for (int jj = 3; jj >= 0; --jj) {
-        __syncthreads();                      // stage input + activation rows in the record
-        __syncthreads();                      // flux pass: final-layer gradients written
-        if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { __syncthreads(); }); }
+        lds_sync();                      // stage input + activation rows in the record
+        lds_sync();                      // flux pass: final-layer gradients written
+        if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { lds_sync(); }); }
         else mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);
       }
     }
-    __syncthreads();                          // tile end: dy0
-    __syncthreads();
+    lds_sync();                          // tile end: dy0
+    lds_sync();
     g0_tile_end<M, W>(A, lds, g0t, tile, lane);
-    __syncthreads();
+    lds_sync();
   }
   // kernel end: dW tiles -> slab; bias row sums of layers >= 1 from the per-trajectory sums
   f4 none[1];
@@ -1741,7 +1753,7 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
       }
     });
   });
-  __syncthreads();                            // bias row sums complete -> bwd_body copies them
+  lds_sync();                            // bias row sums complete -> bwd_body copies them
 }
 
 template <class M>

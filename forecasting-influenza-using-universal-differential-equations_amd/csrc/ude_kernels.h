@@ -267,6 +267,10 @@ struct WRegs {
         });
         if constexpr (BWD) load_x_frags<M, W, d>(rs, lane, wx + M::xq_base(W, d));
       });
+      // wait for the fragments here, once: the loop-carried wait analysis otherwise keeps them
+      // "pending" at the step loop's head and puts a vmcnt(0) before the first MFMA of every
+      // stage, which also drains the loads prefetched a stage ahead (s_waitcnt vmcnt(0))
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     }
   }
 };
@@ -381,6 +385,7 @@ __device__ __forceinline__ void static_hoist(Rsrc rs, const float* lds, f4* c1, 
         c1[M::nz_before(W, k)] = acc;
       }
     });
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // once per tile (see WRegs::load)
   }
 }
 
@@ -1505,8 +1510,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         constexpr bool EARLY_CK = SL == 1;
         if constexpr (CARRY) {
-          // output cotangent loads first: out_finish waits for them with the carried loads
-          // (issued after) still in flight
+          // the step's output cotangents (loaded a stage ago) are consumed before the next stage's
+          // loads are issued: their wait sits in out_finish's runtime loop, where the compiler can
+          // only emit vmcnt(0), which would also drain the fresh prefetch (HBM latency per step)
+          if (next_out) out_finish<M>(A, sc, nstep, n0, gvc, sgn, pgn);
           if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvc);
           if (have_next) {
             ckpt_issue<M>(A, tile, nstep, njj, ckr);
@@ -1563,7 +1570,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (next_out) {
-          out_finish<M>(A, sc, nstep, n0, CARRY ? gvc : gvn, sgn, pgn);
+          if constexpr (!CARRY) out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
           sfor<SL>([&](auto ss) {

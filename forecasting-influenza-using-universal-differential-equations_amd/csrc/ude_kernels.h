@@ -990,14 +990,14 @@ __device__ __forceinline__ void mlp_backward_dw(const float* lds, f4* dw, f4* g0
 // them into shares and handles any further outputs of the step synchronously.
 template <class M>
 __device__ __forceinline__ void out_load(const KArgs& A, const Sched& sc, int o, int n0,
-                                         float (&gv)[M::SLOTS][3]) {
+                                         float (&gv)[M::SLOTS][3], int tid = threadIdx.x) {
   // one source: the full (T, N, R, L) cotangent, or the compact S, I, R one (exactly one of
   // them is set, see ude_rk4_backward_sir)
   const int ld = A.dlatent ? M::L : 3;
   const float* gl = (A.dlatent ? A.dlatent : A.dlat_sir) + (size_t)sc.out_j[o] * A.n_traj * M::R * ld;
   sfor<M::SLOTS>([&](auto ss) {
     constexpr int sl = decltype(ss)::value;
-    const int p = threadIdx.x + sl * NTHREADS;
+    const int p = tid + sl * NTHREADS;
     const int r = p / TT, t = p - r * TT, n = n0 + t;
     const bool valid = p < M::PAIRS && n < A.n_traj;
     const size_t base = valid ? ((size_t)n * M::R + r) * ld : 0;
@@ -1007,13 +1007,13 @@ __device__ __forceinline__ void out_load(const KArgs& A, const Sched& sc, int o,
 }
 template <class M>
 __device__ __forceinline__ void out_issue(const KArgs& A, const Sched& sc, int step, int n0,
-                                          float (&gv)[M::SLOTS][3]) {
-  if (sc.out_start[step] < sc.out_start[step + 1]) out_load<M>(A, sc, sc.out_start[step], n0, gv);
+                                          float (&gv)[M::SLOTS][3], int tid = threadIdx.x) {
+  if (sc.out_start[step] < sc.out_start[step + 1]) out_load<M>(A, sc, sc.out_start[step], n0, gv, tid);
 }
 template <class M>
 __device__ __forceinline__ void out_finish(const KArgs& A, const Sched& sc, int step, int n0,
                                            float (&gv)[M::SLOTS][3], float (&sg)[M::SLOTS][3],
-                                           float (&pg)[M::SLOTS][3]) {
+                                           float (&pg)[M::SLOTS][3], int tid = threadIdx.x) {
 #pragma unroll
   for (int sl = 0; sl < M::SLOTS; ++sl)
 #pragma unroll
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ void out_finish(const KArgs& A, const Sched& sc, int 
   const int o_beg = sc.out_start[step], o_end = sc.out_start[step + 1];
   #pragma unroll 1
   for (int o = o_beg; o < o_end; ++o) {
-    if (o > o_beg) out_load<M>(A, sc, o, n0, gv);
+    if (o > o_beg) out_load<M>(A, sc, o, n0, gv, tid);
     const int mode = sc.out_mode[o];
     const float slope = sc.out_slope[o];
 #pragma unroll
@@ -1039,11 +1039,12 @@ __device__ __forceinline__ void out_finish(const KArgs& A, const Sched& sc, int 
 // Issue the loads of one checkpointed stage input ([f][t] per tile-stage in HBM)
 // into registers, slot sl of thread tid holding pair p = tid + sl * NTHREADS.
 template <class M>
-__device__ __forceinline__ void ckpt_issue(const KArgs& A, int tile, int step, int jj, float (&ck)[M::SLOTS][3]) {
+__device__ __forceinline__ void ckpt_issue(const KArgs& A, int tile, int step, int jj, float (&ck)[M::SLOTS][3],
+                                           int tid = threadIdx.x) {
   const Rsrc rck = make_rsrc(A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0), M::F * TT * 4);
   sfor<M::SLOTS>([&](auto ss) {
     constexpr int sl = decltype(ss)::value;
-    const int p = threadIdx.x + sl * NTHREADS;
+    const int p = tid + sl * NTHREADS;
     const int r = p / TT, t = p - r * TT;
     const int v = (p < M::PAIRS) ? (3 * r * TT + t) * 4 : 0;
 #pragma unroll
@@ -1425,7 +1426,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
             }
           }
         }
-        if (CARRY && have_next && UDE_ABL != 4) {
+        if constexpr (M::SPLIT_BWD) {
+          // stage input, activation rows and output cotangents: the partner waves' (bwd_wbody)
+        } else if (CARRY && have_next && UDE_ABL != 4) {
           constexpr int QR = M::ACT_A4 / 4;
 #pragma unroll
           for (int u = 0; u < act_q_per_thread<M>(); ++u) {
@@ -1509,7 +1512,9 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // wide ones under the flux pass (registers only live across that pass)
         float ckn[SL][3], sgn[SL][3], pgn[SL][3];
         constexpr bool EARLY_CK = SL == 1;
-        if constexpr (CARRY) {
+        if constexpr (M::SPLIT_BWD) {
+          flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
+        } else if constexpr (CARRY) {
           // the step's output cotangents (loaded a stage ago) are consumed before the next stage's
           // loads are issued: their wait sits in out_finish's runtime loop, where the compiler can
           // only emit vmcnt(0), which would also drain the fresh prefetch (HBM latency per step)
@@ -1569,7 +1574,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
-        if (next_out) {
+        if (!M::SPLIT_BWD && next_out) {
           if constexpr (!CARRY) out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
@@ -1720,14 +1725,70 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
 #pragma unroll
   for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
   lds_sync();                            // record zeroed
+  // These waves also move the stage data (the critical-path waves issue no global load in the
+  // stage loop): each stage's checkpointed input and activation rows, loaded one stage ahead into
+  // registers and written into the record at the stage start, and the output cotangents of each
+  // step, loaded a stage ahead and folded into the RK adjoint rows.  Their waits are this wave's
+  // own, so no wait of the critical path can drain the prefetch.
+  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const int wt = threadIdx.x - NTHREADS;                // 0..255: the pair / quad index
+  constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
+  f4 actr[NQ];
+  float ckr[1][3], gvc[1][3];
+  auto put_stage = [&](int tile_) {                     // carried rows -> the record
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int i = wt + u * NTHREADS;
+      if (i < TT * QR) {
+        const int t = i / QR, q = i - t * QR;
+        *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = actr[u];
+      }
+    }
+    if (wt < M::PAIRS) {
+      const int r = wt / TT, t = wt - r * TT;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = ckr[0][c];
+    }
+  };
+  auto get_stage = [&](int tile_, int step_, int jj_) {  // issue one stage's loads
+    ckpt_issue<M>(A, tile_, step_, jj_, ckr, wt);
+    const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile_, step_, jj_));
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int i = wt + u * NTHREADS;
+      if (i < TT * QR) actr[u] = src[i];
+    }
+  };
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
     lds_sync();                          // last step's output cotangents staged
 #pragma unroll
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     lds_sync();
+    bool have = false;
     for (int step = A.n_steps - 1; step >= 0; --step) {
       #pragma unroll 1
       for (int jj = 3; jj >= 0; --jj) {
+        const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
+        if (!have) get_stage(tile, step, jj);           // the tile's first stage
+        put_stage(tile);
+        if (jj == 0 && nstep >= 0) {
+          // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the next step
+          // = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0; read at the step start)
+          float sg[1][3], pg[1][3];
+          out_finish<M>(A, sc, nstep, n0, gvc, sg, pg, wt);
+          if (wt < M::PAIRS) {
+            const int r = wt / TT, t = wt - r * TT;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              lds[t * SR + M::RK_PEND + 3 * r + c] += sg[0][c];
+              lds[t * SR + M::RK_DK3 + 3 * r + c] = pg[0][c];
+            }
+          }
+        }
+        if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvc, wt);
+        have = nstep >= 0;
+        if (have) get_stage(tile, nstep, njj);
         lds_sync();                      // stage input + activation rows in the record
         lds_sync();                      // flux pass: final-layer gradients written
         if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { lds_sync(); }); }

@@ -46,6 +46,8 @@ struct Ops {
     // record + (when it fits) the schedule: up to the full 160 KiB
     HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
     HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, M::SPLIT_FWD>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
     HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
     // the static-feature dy0 kernel stages one tile's (16, R, L) time sums of d latent in LDS
     if (M::HOIST)
@@ -176,8 +178,11 @@ struct Ops {
     a.latent = latent; a.ckpt = ckpt; a.stats_slab = stats_slab;
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
-    const void* kf = ckpt ? (const void*)&ude_fwd_kernel<M, true> : (const void*)&ude_fwd_kernel<M, false>;
-    if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (ckpt && M::SPLIT_FWD && n_tiles <= cus)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F, s, a);
+    else if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;

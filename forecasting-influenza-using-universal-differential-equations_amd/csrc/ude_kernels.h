@@ -429,7 +429,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ============================================================================
 // Forward solve
 // ============================================================================
-template <class M, bool TRAIN, int W>
+template <class M, bool TRAIN, int W, bool SPLIT = false>
 __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
@@ -499,7 +499,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
         mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
-        if constexpr (TRAIN && M::ACT_STORED && UDE_ABL != 11) {
+        if constexpr (TRAIN && M::ACT_STORED && !SPLIT && UDE_ABL != 11) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
@@ -623,14 +623,57 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   }
 }
 
-template <class M, bool TRAIN>
-__global__ __launch_bounds__(NTHREADS, 2) void ude_fwd_kernel(KArgs a) {
+// Training forward of small records (Model::split_fwd): waves 4-7 store each stage's activation
+// rows (the backward's input) from the record to HBM while waves 0-3 run the flux pass; the same
+// barrier sequence as fwd_body.
+template <class M>
+__device__ void fwd_sbody(const KArgs& A, float* lds) {
+  constexpr int SR = M::SR_F;
+  constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
+  const int wt = threadIdx.x - NTHREADS;
+  lds_sync();                                  // record zeroed
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    lds_sync();                                // tile inputs in the record
+    lds_sync();                                // static hoist
+    for (int step = 0; step < A.n_steps; ++step) {
+      #pragma unroll 1
+      for (int j = 0; j < 4; ++j) {
+        sfor<M::D>([&](auto) { lds_sync(); }); // the MLP phases
+        f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
+        f4 v[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+          const int i = wt + u * NTHREADS;
+          if (i < TT * QR) {
+            const int t = i / QR, q = i - t * QR;
+            v[u] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) {
+          const int i = wt + u * NTHREADS;
+          if (i < TT * QR) dst[i] = v[u];
+        }
+        lds_sync();                            // flux pass (the next stage rewrites the rows)
+      }
+    }
+  }
+  lds_sync();                                  // side-statistic reduction
+  lds_sync();
+}
+
+// SPLIT (training, Model::split_fwd, launched when every tile has a CU of its own): 8 waves.
+template <class M, bool TRAIN, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? 2 * NTHREADS : NTHREADS, SPLIT ? 1 : 2) void ude_fwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w == 0) fwd_body<M, TRAIN, 0>(a, lds);
-  else if (w == 1) fwd_body<M, TRAIN, 1>(a, lds);
-  else if (w == 2) fwd_body<M, TRAIN, 2>(a, lds);
-  else fwd_body<M, TRAIN, 3>(a, lds);
+  if constexpr (SPLIT) {
+    if (w >= WAVES) { fwd_sbody<M>(a, lds); return; }
+  }
+  if (w == 0) fwd_body<M, TRAIN, 0, SPLIT>(a, lds);
+  else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT>(a, lds);
+  else if (w == 2) fwd_body<M, TRAIN, 2, SPLIT>(a, lds);
+  else fwd_body<M, TRAIN, 3, SPLIT>(a, lds);
 }
 
 // ============================================================================

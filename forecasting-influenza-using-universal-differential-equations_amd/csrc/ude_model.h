@@ -174,6 +174,10 @@ struct Model {
   // the critical path's gaps.
   static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !BAYES;
   static constexpr int BWD_THREADS = SPLIT_BWD ? 2 * NTHREADS : NTHREADS;
+  // Training forward of small records at one tile per CU: four more waves copy each stage's
+  // activation rows from the record to HBM during the flux pass, off the critical path
+  // (ude_kernels.h fwd_sbody).  With more tiles than CUs two 4-wave workgroups per CU win.
+  static constexpr bool SPLIT_FWD = STORE_ACT && SLOTS_ == 1;
   static constexpr int ACT_STG = X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0);
   static constexpr int LDS_B = (ACT_STG + (STORE_ACT ? TT * ACT_A4 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");

@@ -1449,6 +1449,12 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         // stage input: from the staging slot the previous stage's flux pass filled,
         // or (first stage of the tile) straight from the forward's checkpoint
+        // large records: the step's output cotangents are loaded at its last stage's start, with
+        // the activation rows (their latency is paid there anyway), not right before the flux pass
+        float gvs[M::STORE_ACT_D ? SL : 1][3];
+        if constexpr (M::STORE_ACT_D) {
+          if (jj == 0 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvs);
+        }
         if constexpr (M::STORE_ACT_D && UDE_ABL != 8) {
           // this stage's activation rows straight from the forward's store (issued first: the
           // stage-input copy below runs under their latency)
@@ -1579,7 +1585,6 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
         if constexpr (CARRY) {
         } else if constexpr (M::STORE_ACT_D) {
-          if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
           flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         } else if constexpr (M::STORE_ACT) {
           // the stage's activations are the forward's (staged above); the next stage's are
@@ -1618,7 +1623,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (!M::SPLIT_BWD && next_out) {
-          if constexpr (!CARRY) out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
+          if constexpr (M::STORE_ACT_D) out_finish<M>(A, sc, nstep, n0, gvs, sgn, pgn);
+          else if constexpr (!CARRY) out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
           sfor<SL>([&](auto ss) {

@@ -1821,6 +1821,9 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
         const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
         if (!have) get_stage(tile, step, jj);           // the tile's first stage
         put_stage(tile);
+        lds_sync();                      // stage input + activation rows in the record
+        // the rest runs in the flux interval (these waves' MFMA-free wait), not ahead of the
+        // stage-input barrier, where its dependent scalar schedule loads delayed the critical path
         if (jj == 0 && nstep >= 0) {
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the next step
           // = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0; read at the step start)
@@ -1838,7 +1841,6 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
         if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvc, wt);
         have = nstep >= 0;
         if (have) get_stage(tile, nstep, njj);
-        lds_sync();                      // stage input + activation rows in the record
         lds_sync();                      // flux pass: final-layer gradients written
         if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { lds_sync(); }); }
         else mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);

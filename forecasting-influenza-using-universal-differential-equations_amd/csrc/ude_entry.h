@@ -49,6 +49,12 @@ struct Ops {
     HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, M::SPLIT_FWD>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
     HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, false, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, M::SPLIT_FWD, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_dec_bwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               DecBwdDims<M>::LDS));
     // the static-feature dy0 kernel stages one tile's (16, R, L) time sums of d latent in LDS
     if (M::HOIST)
       HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -104,6 +110,126 @@ struct Ops {
     o->grid_bwd = gb;
     o->lds_fwd = M::LDS_F;
     o->lds_bwd = M::LDS_B;
+    // decoder epilogue (ude_rk4_forward_dec / ude_decoder_backward)
+    int gd = 1;
+    rc = dec_grid(device, n_tiles, &gd);
+    if (rc) return rc;
+    o->dec_pack_bytes = (int64_t)M::DEC_PACK * 4;
+    o->ckpt_final_bytes = (int64_t)n_tiles * M::F * TT * 4;
+    o->dec_ws_bytes = (int64_t)gd * LossDims<M::R>::SLAB * 4;
+    return UDE_OK;
+  }
+
+  static int dec_grid(int device, int n_tiles, int* g) {
+    int rc = ensure_attrs();
+    if (rc) return rc;
+    int cus = 0, occ = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)&ude_dec_bwd_kernel<M>, NTHREADS,
+                                                        DecBwdDims<M>::LDS));
+    if (occ < 1) occ = 1;
+    const long mx = (long)cus * occ;
+    *g = (int)(n_tiles < mx ? n_tiles : mx);
+    if (*g < 1) *g = 1;
+    return UDE_OK;
+  }
+
+  static int dec_pack(const float* W, const float* b, float* out, hipStream_t s) {
+    if (!W || !b || !out) return UDE_E_INVALID;
+    hipLaunchKernelGGL(ude_dec_pack_kernel<M>, dim3((M::DEC_PACK + 255) / 256), dim3(256), 0, s, W, b, out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  // Training forward with the decoder epilogue: y_hat (T, N, R) and latent_init_loss instead of the
+  // latent; ckpt (ckpt_bytes + ckpt_final_bytes) also receives the final state.
+  static int forward_dec(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
+                         const float* dec_pack, float* yhat, float* ckpt, double* stats_slab, double* reg_slab,
+                         float* stats_out, float* reg_out, hipStream_t s) {
+    if (M::BAYES) return UDE_E_UNSUPPORTED;
+    if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !stats_out || !reg_out)
+      return UDE_E_INVALID;
+    if (p->n_steps < 1) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gf = 1, gb = 1;
+    int rc = grids(dev, n_tiles, &gf, &gb);
+    if (rc) return rc;
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
+    a.ckpt = ckpt; a.stats_slab = stats_slab;
+    a.dec_pack = dec_pack; a.yhat = yhat; a.reg_slab = reg_slab;
+    a.ckpt_final = ckpt + ckpt_final_off<M>(n_tiles, p->n_steps);
+    a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
+    a.fa_w = p->fa_w;
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (M::SPLIT_FWD && n_tiles <= cus)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD, true>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F_DEC, s, a);
+    else hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
+    HIPCHK(hipGetLastError());
+    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(ude_sum_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)reg_slab, gf, reg_out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  // Backward of the decoder epilogue: dl3 (T, N, R, 3) for ude_rk4_backward_sir, d W_dec, d b_dec.
+  static int dec_backward(const UdeProblem* p, const void* sched, const float* ckpt, const float* dyhat,
+                          const float* W, const float* grad_reg, void* ws, float* dl3, float* dW, float* db,
+                          hipStream_t s) {
+    if (!sched || !ckpt || !dyhat || !W || !grad_reg || !ws || !dl3 || !dW || !db) return UDE_E_INVALID;
+    if (p->n_steps < 1) return UDE_E_INVALID;
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const int n_tiles = (p->n_traj + TT - 1) / TT;
+    int gd = 1;
+    int rc = dec_grid(dev, n_tiles, &gd);
+    if (rc) return rc;
+    DecBwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.sched = (const unsigned char*)sched; a.ckpt = ckpt; a.dyhat = dyhat; a.W = W; a.grad_reg = grad_reg;
+    a.dl3 = dl3; a.slab = (float*)ws;
+    a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
+    hipLaunchKernelGGL((ude_dec_bwd_kernel<M>), dim3(gd), dim3(NTHREADS), DecBwdDims<M>::LDS, s, a);
+    HIPCHK(hipGetLastError());
+    using D = LossDims<M::R>;
+    hipLaunchKernelGGL((ude_loss_grad_finalize_kernel<D>), dim3((D::SLAB + 63) / 64), dim3(256), 0, s,
+                       (const float*)ws, gd, dW, db);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+
+  // nll_loss over y_hat: ws = musd (T, B, R, 2) floats | per-block fp64 partials
+  static int64_t nll_blocks(int T, int B) { return ((int64_t)T * B * M::R + 255) / 256; }
+  static int64_t nll_part_off(int T, int B) { return (((int64_t)T * B * M::R * 2 * 4) + 255) & ~(int64_t)255; }
+  static int nll_workspace(int T, int S, int B, int64_t* bytes) {
+    if (T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
+    *bytes = nll_part_off(T, B) + nll_blocks(T, B) * 8;
+    return UDE_OK;
+  }
+  static int nll_forward(int T, int S, int B, const float* yhat, const float* y, void* ws, float* out, hipStream_t s) {
+    if (!yhat || !y || !ws || !out || T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
+    const int nb = (int)nll_blocks(T, B);
+    float* musd = (float*)ws;
+    double* part = (double*)((unsigned char*)ws + nll_part_off(T, B));
+    hipLaunchKernelGGL(ude_nll_fwd_kernel<0>, dim3(nb), dim3(256), 0, s, yhat, y, T, S, B, M::R, musd, part);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(ude_nll_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)part, nb,
+                       (double)B * T * M::R, out);
+    HIPCHK(hipGetLastError());
+    return UDE_OK;
+  }
+  static int nll_backward(int T, int S, int B, const float* yhat, const float* y, const float* grad, const void* ws,
+                          float* dyhat, hipStream_t s) {
+    if (!yhat || !y || !grad || !ws || !dyhat || T < 1 || S < 2 || B < 1) return UDE_E_INVALID;
+    hipLaunchKernelGGL(ude_nll_bwd_kernel<0>, dim3((int)nll_blocks(T, B)), dim3(256), 0, s, yhat, y,
+                       (const float*)ws, grad, T, S, B, M::R, dyhat);
+    HIPCHK(hipGetLastError());
     return UDE_OK;
   }
 
@@ -574,6 +700,14 @@ struct Entry {
   int (*rhs_forward)(const UdeProblem*, const float*, const float*, float*, float*, float*, hipStream_t);
   int (*rhs_vjp)(const UdeProblem*, const float*, const float*, const float*, const float*, const float*, float*,
                  void*, float*, hipStream_t);
+  int (*dec_pack)(const float*, const float*, float*, hipStream_t);
+  int (*forward_dec)(const UdeProblem*, const float*, const void*, const float*, const float*, float*, float*, double*,
+                     double*, float*, float*, hipStream_t);
+  int (*dec_backward)(const UdeProblem*, const void*, const float*, const float*, const float*, const float*, void*,
+                      float*, float*, float*, hipStream_t);
+  int (*nll_workspace)(int, int, int, int64_t*);
+  int (*nll_forward)(int, int, int, const float*, const float*, void*, float*, hipStream_t);
+  int (*nll_backward)(int, int, int, const float*, const float*, const float*, const void*, float*, hipStream_t);
 };
 
 template <class M>
@@ -581,7 +715,8 @@ constexpr Entry make_entry() {
   return Entry{&matches<M>, &Ops<M>::query, &Ops<M>::pack, &Ops<M>::pack_bayes, &Ops<M>::forward, &Ops<M>::backward,
                &DopriOps<M>::workspace, &DopriOps<M>::forward, &LossOps<M>::workspace, &LossOps<M>::forward,
                &LossOps<M>::backward, &LossOps<M>::backward_sir, &EvalOps<M>::workspace, &EvalOps<M>::forward,
-               &EvalOps<M>::vjp};
+               &EvalOps<M>::vjp, &Ops<M>::dec_pack, &Ops<M>::forward_dec, &Ops<M>::dec_backward,
+               &Ops<M>::nll_workspace, &Ops<M>::nll_forward, &Ops<M>::nll_backward};
 }
 
 

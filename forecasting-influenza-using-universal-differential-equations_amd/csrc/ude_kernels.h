@@ -11,9 +11,10 @@
 //  * activations live in LDS as one [t][feature] record per trajectory; weights
 //    stream from L2 in a pre-packed fragment order (one 16-B load per lane feeds
 //    4 MFMAs);
-//  * all 4 RK4 stages of every step run inside the launch; the forward saves the
-//    4 stage inputs per step (3R floats each) for the backward, which recomputes
-//    each stage's activations once and back-propagates through the 3/8-rule;
+//  * all 4 RK4 stages of every step run inside the launch; the training forward saves
+//    the 4 stage inputs per step (3R floats each) and each stage's activation rows
+//    (Model::ACT_STORED) for the backward, which reads them back instead of re-running
+//    the forward and back-propagates through the 3/8-rule;
 //  * the parameter gradient dW[o][i] = sum_{t,eval} g[t][o] in[t][i] is another
 //    MFMA GEMM (K = trajectories) whose accumulators stay in each wave's registers
 //    for the whole launch (the wave owns the rows it computed in the forward);
@@ -78,7 +79,16 @@ struct KArgs {
   const float* eslab;         // BAYES backward: the eps stream in slab order, [eval][SLAB_TOTAL]
   const float* dlat_sir;      // backward: the compact S, I, R cotangent (T, N, R, 3) when dlatent is
                               // null (its dims >= 3 all zero); exactly one of the two is set
+  const float* dec_pack;      // DEC forward: decoder fragments + bias (Model::DEC_PACK floats)
+  float* yhat;                // DEC forward: (T, N, R) decoder outputs, written instead of the latent
+  double* reg_slab;           // DEC forward: per-workgroup latent_init_loss partial sums
+  float* ckpt_final;          // DEC training forward: the final-state block (ckpt + ckpt_final_off)
 };
+
+// latent_init_loss summand (lib/train_functions.py:116-126): |x| where x < 0, |1 - x| where x > 1
+__device__ __forceinline__ float reg_term(float v) {
+  return (v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f);
+}
 
 // Timing ablations for a diagnostic build (-DUDE_ABL=n, tools/ablate.py): component n of the
 // small-record backward is skipped (results are wrong; only the kernel time is read).
@@ -163,6 +173,32 @@ __device__ __forceinline__ f4 gemm_tile(Rsrc rs, const float* bp, int lane, f4 a
     acc = mfma4(a[q][1], x[1], acc);
     acc = mfma4(a[q][2], x[2], acc);
     acc = mfma4(a[q][3], x[3], acc);
+  }
+  return acc;
+}
+
+// As gemm_tile with the A fragments in flight QC quads at a time (4 QC VGPRs): for a GEMM outside
+// the stage loop's critical path in a kernel at its register limit (the DEC forward's decoder).
+template <int KP, int WOFF, int QC>
+__device__ __forceinline__ f4 gemm_tile_lean(Rsrc rs, const float* bp, int lane, f4 acc) {
+  constexpr int KQ = KP / 4, NQ = KP / 16;
+  const float* b = bp + (lane >> 4) * KQ;
+#pragma unroll
+  for (int q0 = 0; q0 < NQ; q0 += QC) {
+    f4 a[QC];
+#pragma unroll
+    for (int q = 0; q < QC; ++q)
+      if (q0 + q < NQ) a[q] = ldw(rs, lane * 16, (WOFF + (q0 + q) * 256) * 4);
+#pragma unroll
+    for (int q = 0; q < QC; ++q) {
+      if (q0 + q < NQ) {
+        const f4 x = *reinterpret_cast<const f4*>(b + 4 * (q0 + q));
+        acc = mfma4(a[q][0], x[0], acc);
+        acc = mfma4(a[q][1], x[1], acc);
+        acc = mfma4(a[q][2], x[2], acc);
+        acc = mfma4(a[q][3], x[3], acc);
+      }
+    }
   }
   return acc;
 }
@@ -411,6 +447,13 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
 
+// DEC training forward: the solve's final state y_{n_steps} ([tile][F][16]) behind the stage
+// checkpoints and stored activations (the decoder backward reads every output state from there).
+template <class M>
+__host__ __device__ __forceinline__ size_t ckpt_final_off(int n_tiles, int n_steps) {
+  return (size_t)n_tiles * n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::ACT_A4 : 0));
+}
+
 // Stored activations (Model::STORE_ACT) of one tile-stage: [16][ACT_A4] behind the checkpoint.
 template <class M>
 __device__ __forceinline__ float* act_block(float* ckpt, int n_tiles, int n_steps, int tile, int step, int stage) {
@@ -429,7 +472,12 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ============================================================================
 // Forward solve
 // ============================================================================
-template <class M, bool TRAIN, int W, bool SPLIT = false>
+// DEC (decoder epilogue): instead of the (T, N, R, L) latent, every output time
+// emits y_hat = W_dec . y[:3R] + b_dec ((T, N, R), the Decoder of lib/models.py:27-51 as
+// lib/VAE.py:138 applies it) and the latent_init_loss sum over y[..., :3] (:189); the training
+// forward also stores the final state for the decoder backward.  Outputs must be grid hits
+// (schedule mode 1; the host checks).
+template <class M, bool TRAIN, int W, bool SPLIT = false, bool DEC = false>
 __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
@@ -437,7 +485,12 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
+  const Rsrc rsd = DEC ? make_rsrc(A.dec_pack, M::DEC_PACK * 4) : rs;
   double st_b = 0, st_g = 0, st_bb = 0, st_gg = 0, st_fa = 0;
+  // DEC: this thread's latent_init_loss partial lives in LDS behind the record (the large models'
+  // forward is at its 256-VGPR limit: two more live registers spilled)
+  double* st_reg = reinterpret_cast<double*>(lds + M::REG_LDS_F) + tid;
+  if constexpr (DEC) *st_reg = 0.0;
 
   WRegs<M, W, false> wr;
   wr.load(rs, lane);
@@ -449,6 +502,27 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
     float ys[SL][3], k1[SL][3], k2[SL][3], k3[SL][3];
+    // DEC: y_hat of output jo from the state in the record's Y slot (decoder row tiles over the
+    // waves; no barrier: the next write of the Y slot is behind the next stage's layer barriers)
+    auto dec_emit = [&](int jo) {
+      if constexpr (DEC) {
+        const int t = lane & 15, g = lane >> 4;
+        sfor<M::RTD>([&](auto kk) {
+          constexpr int k = decltype(kk)::value;
+          if constexpr (k % WAVES == W) {
+            f4 acc = ldw(rsd, g * 16, (M::DEC_WF + k * 16) * 4);
+            acc = gemm_tile_lean<M::F16, k * (M::F16 / 16) * 256, 2>(rsd, lds + t * SR + M::Y_OFF, lane, acc);
+            const int n = n0 + t;
+            if (n < A.n_traj) {
+              float* dst = A.yhat + ((size_t)jo * A.n_traj + n) * M::R + k * 16 + 4 * g;
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (k * 16 + 4 * g + e < M::R) dst[e] = acc[e];
+            }
+          }
+        });
+      }
+    };
 
     // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
     sfor<SL>([&](auto ss) {
@@ -464,8 +538,9 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
           ys[sl][c] = valid ? src[c] : 0.f;
           lds[t * SR + M::Y_OFF + 3 * r + c] = ys[sl][c];
           if (TRAIN && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
+          if (DEC && valid) *st_reg += (double)reg_term(ys[sl][c]);
         }
-        if (valid) {
+        if (valid && !DEC) {
           float* dst = A.latent + ((size_t)n * M::R + r) * M::L;
           for (int c = 0; c < M::L; ++c) dst[c] = src[c];
         }
@@ -473,7 +548,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     });
     // static latent dims (zero derivative, carried unchanged: lib/models.py:144) of every output
     // time, once per tile (not in the step loop, where each copy waited on a global load)
-    if constexpr (M::L > 3) {
+    if constexpr (M::L > 3 && !DEC) {
       #pragma unroll 1
       for (int i = tid; i < A.n_out * M::PAIRS; i += NTHREADS) {
         const int o = i / M::PAIRS, p = i - o * M::PAIRS;
@@ -491,6 +566,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
     static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
     lds_sync();
+    if constexpr (DEC) dec_emit(0);               // output 0 = y0
 
     for (int step = 0; step < A.n_steps; ++step) {
       const float dt = sc.dt[step];
@@ -571,7 +647,18 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
                 ys[sl][c] = ys[sl][c] + dy;
                 Yn[c] = ys[sl][c];
               }
-              if (valid) {
+              if constexpr (DEC) {
+                // every output is a grid hit (mode 1): latent_init_loss of the new state; y_hat
+                // follows from the record after the barrier (dec_emit)
+                if (valid && sc.out_start[step] < sc.out_start[step + 1]) {
+#pragma unroll
+                  for (int c = 0; c < 3; ++c) *st_reg += (double)reg_term(ys[sl][c]);
+                }
+                if (TRAIN && step == A.n_steps - 1) {
+#pragma unroll
+                  for (int c = 0; c < 3; ++c) A.ckpt_final[((size_t)tile * M::F + 3 * r + c) * TT + t] = ys[sl][c];
+                }
+              } else if (valid) {
                 const int o_end = sc.out_start[step + 1];
                 #pragma unroll 1
                 for (int o = sc.out_start[step]; o < o_end; ++o) {
@@ -604,22 +691,28 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         });
         lds_sync();
       }
+      if constexpr (DEC) {
+        if (sc.out_start[step] < sc.out_start[step + 1]) dec_emit(sc.out_j[sc.out_start[step]]);
+      }
     }
   }
 
   // deterministic per-workgroup partial sums
+  constexpr int NS = DEC ? 6 : 5;
   double* red = reinterpret_cast<double*>(lds);
-  double v[5] = {wave_sum(st_b), wave_sum(st_g), wave_sum(st_bb), wave_sum(st_gg), wave_sum(st_fa)};
+  double v[6] = {wave_sum(st_b), wave_sum(st_g), wave_sum(st_bb), wave_sum(st_gg), wave_sum(st_fa),
+                 DEC ? wave_sum(*st_reg) : 0.0};
   lds_sync();
   if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < 5; ++c) red[(tid >> 6) * 5 + c] = v[c];
+    for (int c = 0; c < NS; ++c) red[(tid >> 6) * NS + c] = v[c];
   }
   lds_sync();
-  if (tid < 5) {
+  if (tid < NS) {
     double s = 0;
-    for (int w = 0; w < WAVES; ++w) s += red[w * 5 + tid];
-    A.stats_slab[(size_t)blockIdx.x * 5 + tid] = s;
+    for (int w = 0; w < WAVES; ++w) s += red[w * NS + tid];
+    if (tid < 5) A.stats_slab[(size_t)blockIdx.x * 5 + tid] = s;
+    else A.reg_slab[blockIdx.x] = s;
   }
 }
 
@@ -663,17 +756,18 @@ __device__ void fwd_sbody(const KArgs& A, float* lds) {
 }
 
 // SPLIT (training, Model::split_fwd, launched when every tile has a CU of its own): 8 waves.
-template <class M, bool TRAIN, bool SPLIT = false>
+// DEC: the decoder epilogue (y_hat and latent_init_loss, no latent).
+template <class M, bool TRAIN, bool SPLIT = false, bool DEC = false>
 __global__ __launch_bounds__(SPLIT ? 2 * NTHREADS : NTHREADS, SPLIT ? 1 : 2) void ude_fwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (SPLIT) {
     if (w >= WAVES) { fwd_sbody<M>(a, lds); return; }
   }
-  if (w == 0) fwd_body<M, TRAIN, 0, SPLIT>(a, lds);
-  else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT>(a, lds);
-  else if (w == 2) fwd_body<M, TRAIN, 2, SPLIT>(a, lds);
-  else fwd_body<M, TRAIN, 3, SPLIT>(a, lds);
+  if (w == 0) fwd_body<M, TRAIN, 0, SPLIT, DEC>(a, lds);
+  else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT, DEC>(a, lds);
+  else if (w == 2) fwd_body<M, TRAIN, 2, SPLIT, DEC>(a, lds);
+  else fwd_body<M, TRAIN, 3, SPLIT, DEC>(a, lds);
 }
 
 // ============================================================================
@@ -1986,6 +2080,22 @@ __global__ __launch_bounds__(256) void ude_pack_kernel(PackPtrs P, float* __rest
   }
 }
 
+// Decoder Linear(3R -> R) (lib/models.py:39) -> the DEC epilogue's fragment layout (Model::DEC_PACK).
+template <class M>
+__global__ __launch_bounds__(256) void ude_dec_pack_kernel(const float* __restrict__ Wd, const float* __restrict__ bd,
+                                                           float* __restrict__ out) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx < M::DEC_WF) {
+    constexpr int KQ = M::F16 / 4, NQ = M::F16 / 16;
+    const int e = idx & 3, ln = (idx >> 2) & 63, q = (idx >> 8) % NQ, rt = (idx >> 8) / NQ;
+    const int o = rt * 16 + (ln & 15), f = (ln >> 4) * KQ + 4 * q + e;
+    out[idx] = (o < M::R && f < M::F) ? Wd[(size_t)o * M::F + f] : 0.f;
+  } else if (idx < M::DEC_PACK) {
+    const int o = idx - M::DEC_WF;
+    out[idx] = o < M::R ? bd[o] : 0.f;
+  }
+}
+
 // ============================================================================
 // Deterministic reductions over the per-workgroup partials
 // ============================================================================
@@ -2233,6 +2343,17 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
         dy0[((size_t)n * M::R + r) * M::L + 3 + cc] = acc[j][e] + tsum[((4 * g + e) * M::R + r) * M::L + 3 + cc];
     }
   }
+}
+
+// fixed-order sum of per-workgroup fp64 partials -> one float (latent_init_loss of the DEC forward)
+template <int V_ = 0>
+__global__ void ude_sum_finalize_kernel(const double* __restrict__ part, int n, float* __restrict__ out) {
+  const int ln = threadIdx.x;
+  double s = 0.0;
+  for (int i = ln; i < n; i += 64) s += part[i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (ln == 0) out[0] = (float)s;
 }
 
 template <int V_ = 0>

@@ -64,10 +64,6 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__device__ __forceinline__ float reg_term(float v) {
-  return (v < 0.f ? fabsf(v) : 0.f) + (v > 1.f ? fabsf(1.f - v) : 0.f);
-}
-
 // LDS layout: X [SP][XS] | Wl [NP][XS] | P [SP][PS] (Q in place, backward) | bias [NP] | aux [NP]
 // A group's rows are read once: when L % 4 == 0 the dims 0..3 of every (sample, region)
 // are one 16-B load, and the next group's loads are issued into registers before the
@@ -455,6 +451,228 @@ __global__ __launch_bounds__(256) void ude_loss_grad_finalize_kernel(const float
       if (o < D::R) db[o] = v;
     }
   }
+}
+
+
+// ============================================================================
+// Decoder epilogue backward and the nll over y_hat
+// ============================================================================
+// With the DEC forward (ude_kernels.h fwd_body<..., DEC>) the training solve emits
+// y_hat (T, N, R) = Decoder(latent[..., :3]) and sum latent_init_loss(latent[..., :3]) directly and
+// never writes the latent.  Backward of that epilogue, given d y_hat (from nll_loss or any other
+// consumer of y_pred) and g_reg = d loss / d latent_init_loss:
+//   d y[t, n, :3R] = W_dec^T d y_hat[t, n, :] + g_reg * latent_init_loss'(y)   (the compact S, I, R
+//                    cotangent ude_rk4_backward_sir consumes)
+//   d W_dec = sum_{t, n} d y_hat[t, n, :] y[t, n, :3R]^T,  d b_dec = sum_{t, n} d y_hat[t, n, :]
+// Every output state y is read from the training forward's own store (stage-0 checkpoint of its
+// grid step, or the final-state block): no latent exists.  One workgroup (4 waves) walks trajectory
+// tiles; per (tile, output) the y block ([3R][16], contiguous in the checkpoint) and the d y_hat rows
+// go to LDS and both GEMMs run on v_mfma_f32_16x16x4_f32; d W_dec stays in registers (deterministic
+// per-workgroup slabs, summed by ude_loss_grad_finalize_kernel).
+struct DecBwdArgs {
+  const unsigned char* sched;
+  const float* ckpt;       // training-forward store: stage checkpoints (+ activations) + final block
+  const float* dyhat;      // (T, N, R)
+  const float* W;          // (R, 3R)
+  const float* grad_reg;   // device scalar: d loss / d latent_init_loss
+  float* dl3;              // (T, N, R, 3)
+  float* slab;             // [grid][LossDims<R>::SLAB]
+  int n_traj, n_steps, n_out, n_tiles;
+};
+
+template <class M>
+struct DecBwdDims {
+  using D = LossDims<M::R>;
+  static constexpr int KP = D::KP, NP = D::NP;        // 3R and R padded to 16
+  static constexpr int WS = NP + 4, DS = NP + 4, YS = KP + 4;
+  static constexpr int NFT = KP / 16, NRT = NP / 16;
+  static constexpr int NDW = NFT * NRT;                // dW tiles (r tile, f tile)
+  static constexpr int dw_of(int w) { return (NDW + WAVES - 1 - w) / WAVES; }
+  static constexpr int LDS = (KP * WS + TT * YS + TT * DS + TT * YS) * 4;
+};
+
+template <class M, int W>
+__device__ void dec_bwd_body(const DecBwdArgs& A, float* lds) {
+  using Q = DecBwdDims<M>;
+  constexpr int F = M::F, R = M::R;
+  const int tid = threadIdx.x, lane = tid & 63, t16 = lane & 15, g = lane >> 4;
+  float* Wl = lds;                       // [KP][WS]  W^T: Wl[f][r] = W[r][f]
+  float* Yt = Wl + Q::KP * Q::WS;        // [16][YS]  output state y[t][f]
+  float* Dy = Yt + TT * Q::YS;           // [16][DS]  d y_hat[t][r]
+  float* Cs = Dy + TT * Q::DS;           // [16][YS]  d y[t][f] staging
+  const Sched sc(A.sched, A.n_steps, A.n_out);
+  const float g_reg = *A.grad_reg;
+  #pragma unroll 1
+  for (int i = tid; i < Q::KP * Q::WS; i += NTHREADS) {
+    const int f = i / Q::WS, r = i - f * Q::WS;
+    Wl[i] = (f < F && r < R) ? A.W[(size_t)r * F + f] : 0.f;
+  }
+  #pragma unroll 1
+  for (int i = tid; i < TT * Q::YS; i += NTHREADS) Yt[i] = 0.f;
+  #pragma unroll 1
+  for (int i = tid; i < TT * Q::DS; i += NTHREADS) Dy[i] = 0.f;
+  f4 dw[Q::dw_of(W) > 0 ? Q::dw_of(W) : 1];
+#pragma unroll
+  for (int i = 0; i < Q::dw_of(W); ++i) dw[i] = f4zero();
+  float db = 0.f;                        // thread r < NP: d b_dec partial
+  const size_t fin = ckpt_final_off<M>(A.n_tiles, A.n_steps);
+
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    const int n0 = tile * TT;
+    const int nv = min(TT, A.n_traj - n0);
+    // outputs in order: output 0 at grid point 0, then each step's (mode 1) output at step + 1
+    int step = -1, o = 0;
+    #pragma unroll 1
+    while (true) {
+      int jo, k;
+      if (step < 0) {
+        jo = 0; k = 0; step = 0; o = sc.out_start[0];
+      } else {
+        while (step < A.n_steps && o >= sc.out_start[step + 1]) ++step;
+        if (step >= A.n_steps) break;
+        jo = sc.out_j[o]; k = step + 1; ++o;
+      }
+      __syncthreads();                   // previous output's Cs copied, Yt / Dy reads done
+      // y block [F][16] of grid point k -> Yt[t][f]; d y_hat rows -> Dy[t][r]
+      const float* yb = k < A.n_steps ? A.ckpt + ckpt_index(tile, A.n_steps, k, 0, F, 0, 0)
+                                      : A.ckpt + fin + (size_t)tile * F * TT;
+      #pragma unroll 4
+      for (int i = tid; i < F * TT; i += NTHREADS) {
+        const int f = i >> 4, t = i & 15;
+        Yt[t * Q::YS + f] = yb[i];
+      }
+      const float* dyr = A.dyhat + ((size_t)jo * A.n_traj + n0) * R;
+      #pragma unroll 4
+      for (int i = tid; i < TT * R; i += NTHREADS) {
+        const int t = i / R, r = i - t * R;
+        Dy[t * Q::DS + r] = t < nv ? dyr[i] : 0.f;
+      }
+      __syncthreads();
+      // d W_dec tiles (rows r, cols f; K = the tile's 16 trajectories) and d b_dec
+#pragma unroll
+      for (int i = 0; i < Q::dw_of(W); ++i) {
+        const int id = W + WAVES * i, rt = id / Q::NFT, ft = id - rt * Q::NFT;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dw[i] = mfma4(Dy[(4 * q + g) * Q::DS + rt * 16 + t16], Yt[(4 * q + g) * Q::YS + ft * 16 + t16], dw[i]);
+      }
+      if (tid < Q::NP) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) db += Dy[t * Q::DS + tid];
+      }
+      // d y^T tiles (rows f, cols t; K = the R decoder outputs) + latent_init_loss'
+      for (int ft = W; ft < Q::NFT; ft += WAVES) {
+        f4 acc = f4zero();
+#pragma unroll
+        for (int q = 0; q < Q::NP / 4; ++q)
+          acc = mfma4(Wl[(ft * 16 + t16) * Q::WS + 4 * q + g], Dy[t16 * Q::DS + 4 * q + g], acc);
+        const f4 y = *reinterpret_cast<const f4*>(Yt + t16 * Q::YS + ft * 16 + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += g_reg * (y[e] < 0.f ? -1.f : (y[e] > 1.f ? 1.f : 0.f));
+        *reinterpret_cast<f4*>(Cs + t16 * Q::YS + ft * 16 + 4 * g) = acc;
+      }
+      __syncthreads();
+      // the tile's (16, 3R) block of d latent[..., :3] at output jo is contiguous
+      float* dst = A.dl3 + ((size_t)jo * A.n_traj + n0) * F;
+      #pragma unroll 4
+      for (int i = tid; i < nv * F; i += NTHREADS) {
+        const int t = i / F, f = i - t * F;
+        dst[i] = Cs[t * Q::YS + f];
+      }
+    }
+  }
+  float* my = A.slab + (size_t)blockIdx.x * LossDims<R>::SLAB;
+#pragma unroll
+  for (int i = 0; i < Q::dw_of(W); ++i) {
+    const int id = W + WAVES * i, rt = id / Q::NFT, ft = id - rt * Q::NFT;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) my[(rt * 16 + 4 * g + e) * Q::KP + ft * 16 + t16] = dw[i][e];
+  }
+  if (tid < Q::NP) my[Q::NP * Q::KP + tid] = db;
+}
+
+template <class M>
+__global__ __launch_bounds__(NTHREADS) void ude_dec_bwd_kernel(DecBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w == 0) dec_bwd_body<M, 0>(a, lds);
+  else if (w == 1) dec_bwd_body<M, 1>(a, lds);
+  else if (w == 2) dec_bwd_body<M, 2>(a, lds);
+  else dec_bwd_body<M, 3>(a, lds);
+}
+
+// nll_loss over y_hat (lib/train_functions.py:81-90 on y_pred = y_hat.reshape(T, S, B, R)
+// .permute(2, 1, 0, 3), lib/VAE.py:138): one thread per (t, b, r) group, its S samples
+// y_hat[t, s*B + b, r] (coalesced across the group's neighbours for every s).  fp64 sums: mean and
+// unbiased std of the samples, -Normal(mu, sd).log_prob(y) where y != -1, mean over B*T*R
+// (per-block partials, fixed-order finalize).  musd (T, B, R, 2) is kept for the backward.
+template <int V_ = 0>
+__global__ __launch_bounds__(256) void ude_nll_fwd_kernel(const float* __restrict__ yhat, const float* __restrict__ y,
+                                                          int T, int S, int B, int R, float* __restrict__ musd,
+                                                          double* __restrict__ part) {
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int ngr = T * B * R;
+  double acc = 0.0;
+  if (gid < ngr) {
+    const int r = gid % R, tb = gid / R, b = tb % B, t = tb / B;
+    const size_t stride = (size_t)B * R;
+    const float* p = yhat + (size_t)t * S * stride + (size_t)b * R + r;
+    double s1 = 0.0;
+    for (int s = 0; s < S; ++s) s1 += (double)p[s * stride];
+    const float mu = (float)(s1 / (double)S);
+    double s2 = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const float d = p[s * stride] - mu;
+      s2 += (double)(d * d);
+    }
+    const float sd = sqrtf((float)(s2 / (double)(S - 1)));
+    musd[(size_t)gid * 2] = mu;
+    musd[(size_t)gid * 2 + 1] = sd;
+    const float yv = y[((size_t)b * T + t) * R + r];
+    if (yv != -1.f) {
+      const float z = (yv - mu) / sd;
+      acc = (double)(0.5f * z * z + logf(sd) + 0.9189385332046727f);
+    }
+  }
+  __shared__ double red[4];
+  double v = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int V_ = 0>
+__global__ void ude_nll_finalize_kernel(const double* __restrict__ part, int n, double M, float* __restrict__ out) {
+  const int ln = threadIdx.x;
+  double s = 0.0;
+  for (int i = ln; i < n; i += 64) s += part[i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (ln == 0) out[0] = (float)(s / M);
+}
+
+// d nll / d y_hat[t, s*B + b, r] = g_nll / (B T R) * (d mu / S + d sd (y_hat - mu) / ((S - 1) sd))
+template <int V_ = 0>
+__global__ __launch_bounds__(256) void ude_nll_bwd_kernel(const float* __restrict__ yhat, const float* __restrict__ y,
+                                                          const float* __restrict__ musd, const float* __restrict__ grad,
+                                                          int T, int S, int B, int R, float* __restrict__ dyhat) {
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  if (gid >= T * B * R) return;
+  const int r = gid % R, tb = gid / R, b = tb % B, t = tb / B;
+  const float mu = musd[(size_t)gid * 2], sd = musd[(size_t)gid * 2 + 1];
+  const float yv = y[((size_t)b * T + t) * R + r];
+  float cm = 0.f, cs = 0.f;
+  if (yv != -1.f) {
+    const float iv = 1.f / sd, dy = yv - mu;
+    const float dmu = -dy * iv * iv;
+    const float dsd = iv - dy * dy * iv * iv * iv;
+    const float sc = (float)((double)grad[0] / ((double)B * T * R));
+    cm = sc * dmu / (float)S;
+    cs = sc * dsd * iv / (float)(S - 1);
+  }
+  const size_t stride = (size_t)B * R;
+  const size_t base = (size_t)t * S * stride + (size_t)b * R + r;
+  for (int s = 0; s < S; ++s) dyhat[base + s * stride] = cm + cs * (yhat[base + s * stride] - mu);
 }
 
 }  // namespace ude

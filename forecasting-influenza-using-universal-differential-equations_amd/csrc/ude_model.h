@@ -354,6 +354,19 @@ struct Model {
   static constexpr int N_GRAD = N_PARAMS * (BAYES ? 2 : 1);
   static constexpr int PAIRS = R * TT;
   static constexpr int SLOTS = (PAIRS + NTHREADS - 1) / NTHREADS;
+
+  // ---- decoder epilogue (lib/models.py:27-51 Decoder = Linear(3R -> R) on
+  // latent[..., :3], lib/VAE.py:138) ------------------------------------------------------
+  // The training forward can emit y_hat = W_dec . y[:3R] + b_dec at every output time instead of
+  // the (T, N, R, L) latent: one more small GEMM out[o][t] = W_dec[o][:] . Y[t][:] over the
+  // record's Y slot (its 3R features are exactly the decoder's flattened (R, 3) input order).
+  // Packed like a forward layer: [RTD][F16/16][64 lanes][4] fragments, then the bias [RTD * 16].
+  static constexpr int RTD = pad16(R) / 16;
+  static constexpr int DEC_WF = RTD * (F16 / 16) * 256;
+  static constexpr int DEC_PACK = DEC_WF + RTD * 16;
+  // DEC forward: per-thread fp64 latent_init_loss partials behind the forward record
+  static constexpr int REG_LDS_F = TT * SR_F;
+  static constexpr int LDS_F_DEC = LDS_F + NTHREADS * 8;
 };
 
 }  // namespace ude

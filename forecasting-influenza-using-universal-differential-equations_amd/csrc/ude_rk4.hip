@@ -154,6 +154,53 @@ int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, c
   return e->rhs_vjp(p, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, (hipStream_t)stream);
 }
 
+int ude_pack_decoder(const UdeModelDesc* m, const float* W_dec, const float* b_dec, float* dec_pack,
+                     ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  return e->dec_pack(W_dec, b_dec, dec_pack, (hipStream_t)stream);
+}
+
+int ude_rk4_forward_dec(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                        const float* y0, const float* dec_pack, float* yhat, float* ckpt, double* stats_slab,
+                        double* reg_slab, float* stats_out, float* reg_out, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 1) return UDE_E_INVALID;
+  return e->forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, stats_out, reg_out,
+                        (hipStream_t)stream);
+}
+
+int ude_decoder_backward(const UdeModelDesc* m, const UdeProblem* p, const void* sched, const float* ckpt,
+                         const float* dyhat, const float* W_dec, const float* grad_reg, void* ws, float* dl3,
+                         float* dW_dec, float* db_dec, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 1) return UDE_E_INVALID;
+  return e->dec_backward(p, sched, ckpt, dyhat, W_dec, grad_reg, ws, dl3, dW_dec, db_dec, (hipStream_t)stream);
+}
+
+int ude_nll_workspace(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, int64_t* ws_bytes) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!ws_bytes) return UDE_E_INVALID;
+  return e->nll_workspace(T, S, B, ws_bytes);
+}
+
+int ude_nll_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* yhat, const float* y,
+                    void* ws, float* out, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  return e->nll_forward(T, S, B, yhat, y, ws, out, (hipStream_t)stream);
+}
+
+int ude_nll_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* yhat, const float* y,
+                     const float* grad, const void* ws, float* dyhat, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  return e->nll_backward(T, S, B, yhat, y, grad, ws, dyhat, (hipStream_t)stream);
+}
+
 #ifdef UDE_PROFILE
 void ude_debug_set_prof(unsigned long long* p) { ude::g_prof_buffer = p; }
 #endif

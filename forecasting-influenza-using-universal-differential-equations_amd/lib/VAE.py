@@ -7,9 +7,21 @@ when the model lives on a HIP device -- then decodes ``latent[..., :3]``.
 ``calc_loss`` (:142-198) reads the solver's side outputs exactly as the
 reference does (``ode.posterior()``, ``torch.norm(torch.stack(ode.tracker))``,
 ``self.latent``) and ``train_step`` (:200-223) back-propagates through the solve.
-On a HIP device the ``nll`` and ``reg_loss`` terms of the model's own training
-prediction come from the fused loss head (ude_amd/loss_head.py: decoder +
-nll_loss + latent_init_loss, forward and backward in one kernel pass each).
+Under ``torch.distributed`` (one process per GPU, ``VAE.enable_data_parallel()`` or a process
+group of more than one rank at ``setup_training``) ``train_step`` runs data-parallel (BASELINE
+configs[4]): each rank takes a contiguous shard of the batch's windows, the
+posterior / |Fa| side statistics are made global before ``calc_loss``
+(``ude_amd.distributed.sync_side_stats``), every loss term is weighted by its share of the
+global batch, and one bucketed all-reduce of the encoder + ODE + decoder gradients precedes
+the grad-norm gate, so every rank takes the identical Adam step the single-process run takes.
+On a HIP device a training call runs the solve with the decoder epilogue
+(ude_amd/decoder_head.py): the forward kernel emits the decoder output
+y_hat = Decoder(latent[..., :3]) and latent_init_loss(latent[..., :3]) at every output time and
+writes no (T, N, R, L) latent -- ``self.latent`` is rebuilt from the training store only when it
+is read -- and calc_loss takes nll_loss of that prediction from the gfx950 nll kernels.  When
+the epilogue does not apply (output times between grid points, Bayesian RHS, a non-reference
+decoder) the latent is written and the fused loss head (ude_amd/loss_head.py: decoder +
+nll_loss + latent_init_loss in one kernel pass each) serves the same terms.
 """
 from itertools import chain
 
@@ -24,6 +36,8 @@ import lib.Metrics as Metrics
 import lib.models as models
 import lib.train_functions as train_functions
 from lib.in_development.models_bayes import Dense_Variational
+from ude_amd import decoder_head
+from ude_amd import distributed as udist
 from ude_amd import loss_head
 
 
@@ -76,6 +90,20 @@ class VAE:
         self.prior_params = prior_params
         self.started = False
         self.skip_count = 0
+        self._dp = None            # data-parallel state (enable_data_parallel)
+        self._dp_eps = None        # (full window count, lo, hi) while a sharded step draws eps
+
+    # ``latent``: a tensor, or (decoder-epilogue training solve) rebuilt on first read
+    @property
+    def latent(self):
+        v = self.__dict__.get("_latent")
+        if isinstance(v, decoder_head.LazyLatent):
+            return v.get()
+        return v
+
+    @latent.setter
+    def latent(self, value):
+        self.__dict__["_latent"] = value
 
     def to(self, device):
         """Move encoder / ODE / decoder (the reference pins 'cpu'; here a HIP device runs the fused solve)."""
@@ -97,12 +125,35 @@ class VAE:
         return chain(self.enc.parameters(), self.ode.parameters(), self.dec.parameters())
 
     def setup_training(self, lr=1e-3):
+        if self._dp is None and udist.world_size() > 1:
+            self.enable_data_parallel()
         self.optimizer = torch.optim.Adam(self.parameters(), lr=lr)
         self._history = train_functions.history()
 
+    def enable_data_parallel(self, group=None):
+        """Data-parallel training steps over the default (or given) process group: rank 0's
+        weights are broadcast so every replica starts identical; ``train_step`` then shards
+        each batch's windows over the ranks (see the module docstring)."""
+        self._dp = {"group": group, "world": udist.world_size(group), "rank": udist.rank(group)}
+        udist.broadcast_parameters(self.parameters(), group=group)
+        return self
+
+    def _shard(self, B):
+        """This rank's contiguous window range [lo, hi) of a B-window batch."""
+        world, rank = self._dp["world"], self._dp["rank"]
+        base, rem = divmod(B, world)
+        lo = rank * base + min(rank, rem)
+        return lo, lo + base + (1 if rank < rem else 0)
     def __call__(self, x, t, n_samples=32, training=False):
         B = x.shape[0]
-        eps = torch.randn(n_samples, B, self.n_regions, self.ld_enc, dtype=self.dtype, device=self.device)
+        if self._dp_eps is not None:
+            # sharded step: the full batch's eps (same draw on every rank) sliced to this shard, so
+            # the data-parallel step sees exactly the single-process step's samples
+            b_full, lo, hi = self._dp_eps
+            eps = torch.randn(n_samples, b_full, self.n_regions, self.ld_enc, dtype=self.dtype,
+                              device=self.device)[:, lo:hi]
+        else:
+            eps = torch.randn(n_samples, B, self.n_regions, self.ld_enc, dtype=self.dtype, device=self.device)
         self.ode.clear_tracking()
         if training:
             self.optimizer.zero_grad()
@@ -115,19 +166,40 @@ class VAE:
                 n_samples = 1
                 self.mean = self.enc(x)
                 z = (models.reparam(eps, None, self.mean, n_samples, B, uncertainty=False) + 1e-5).unsqueeze(1)
+            dec = None
+            if training and decoder_head.eligible(self.ode, z, decoder_head.decoder_linear(self.dec)):
+                dec = decoder_head.solve_decode(self.ode, z, t, step, decoder_head.decoder_linear(self.dec))
+            if dec is not None:
+                # y_hat (T, N, R) == self.dec(latent[..., :3]) (lib/models.py:45-51), no latent written
+                yhat, reg, lazy, _ = dec
+                self.latent = lazy
+                y_pred = yhat.reshape((-1, n_samples, B, self.n_regions)).permute(2, 1, 0, 3)
+                self._pred_src = (y_pred, n_samples, B, yhat, reg)
+                return y_pred
             self.latent = odeint(self.ode, z, t, method="rk4", options=dict(step_size=step))
             decoded = self.dec(self.latent[..., :3])
             y_pred = decoded.reshape((-1, n_samples, B, self.n_regions)).permute(2, 1, 0, 3)
         # calc_loss may take nll / reg from the fused loss head when handed this prediction
-        self._pred_src = (y_pred, n_samples, B) if training else None
+        self._pred_src = (y_pred, n_samples, B, None, None) if training else None
         return y_pred
 
     def _fused_head(self, y_pred, y_true, losses):
-        """(nll, reg) from the fused gfx950 loss head (ude_amd/loss_head.py), or None when
-        y_pred is not this model's latest training prediction or the shapes do not fit."""
+        """(nll, reg, per-group prediction mean / std) for this model's latest training prediction:
+        from the decoder-epilogue solve (reg) and the gfx950 nll kernels, or from the fused loss
+        head over the written latent (ude_amd/loss_head.py); None when y_pred is not that
+        prediction or the shapes do not fit."""
         src = getattr(self, "_pred_src", None)
         if not (losses.get("nll", True) or losses.get("reg_loss", True)) or src is None or src[0] is not y_pred:
             return None
+        if src[3] is not None:
+            yhat, reg = src[3], src[4]
+            if losses.get("nll", True) and src[1] >= 2:
+                nll, musd = decoder_head.nll_head(self.ode, yhat, y_true, src[1], src[2])
+            elif losses.get("nll", True):
+                return None
+            else:
+                nll, musd = None, None
+            return nll, reg, musd
         lin = self.dec.decoder[-1]
         if getattr(self.dec, "latent_dim", None) != 3 or not hasattr(self.ode, "ude_config"):
             return None
@@ -150,6 +222,11 @@ class VAE:
                                  "constraints Real() / GreaterThan(lower_bound=0.0), but found invalid values")
 
     def calc_loss(self, y_pred, y_true, losses):
+        """The reference's loss composition (:142-198).  In a data-parallel step
+        (``self._dp_w``) each term is weighted by this rank's share of the global loss -- batch
+        means by the window fraction, sums by 1, terms of the (already global) side statistics and
+        of the parameters by 1/world -- and the reported values are the all-reduced global ones."""
+        dpw = getattr(self, "_dp_w", None)
         terms = {}
         if losses.get("anneal", True):
             self.tr_step += 1
@@ -158,10 +235,15 @@ class VAE:
             terms["mse"] = torch.mean(torch.square(y_pred - y_true.unsqueeze(1)))
         fused = self._fused_head(y_pred, y_true, losses)
         checks = []
-        if fused is not None:
+        if fused is not None and losses.get("nll", True):
+            # nll_loss builds Normal(y_mean, y_std) only when the nll term is on (ref :160-161)
             checks.append(("nll_loss prediction mean / std", fused[2][..., 0], fused[2][..., 1]))
+        if fused is None and losses.get("reg_loss", True) and getattr(self, "_pred_src", None) is not None \
+                and self._pred_src[0] is y_pred and self._pred_src[4] is not None:
+            fused = (None, self._pred_src[4], None)     # reg of the decoder-epilogue solve (nll eager)
         if losses.get("nll", True):
-            terms["nll"] = fused[0] if fused is not None else train_functions.nll_loss(y_pred, y_true)
+            terms["nll"] = fused[0] if (fused is not None and fused[0] is not None) \
+                else train_functions.nll_loss(y_pred, y_true)
         if losses.get("kl_z", True):
             prior = models.make_prior(self.mean, latent_dim=self.ld_ode, device=self.device)
             kl = train_functions.kl_divergence(prior, Normal(self.mean, self.std)).sum(-1).mean()
@@ -183,23 +265,59 @@ class VAE:
         if self.ode.uncertainty == "bayes":
             terms["ode_kl"] = self.ode_kl_w * self.ode.get_kl()
         self._validate_normals(checks)
+        if dpw is not None:
+            frac, glob = dpw
+            kind = {"mse": frac, "nll": frac, "kl_latent": frac, "reg_loss": 1.0}
+            terms = {k: v * kind.get(k, glob) for k, v in terms.items()}
         loss = torch.tensor(0.0, requires_grad=True)
         for v in terms.values():
             loss = loss + v
-        names, data = ["loss"], [round(loss.cpu().item(), 3)]
+        shown = {k: (norm if k == "Fa_norm" else v) for k, v in terms.items()}
+        if dpw is not None:
+            # global values for the history: one all-reduce of the weighted terms (the Fa norm
+            # is already global)
+            keys = list(terms)
+            vec = torch.stack([loss.detach().reshape(()).to(torch.float64)] +
+                              [terms[k].detach().reshape(()).to(torch.float64) for k in keys]).to(self.device)
+            vec = udist.all_reduce_values(vec, group=self._dp["group"])
+            loss_val = vec[0]
+            shown = {k: (norm if k == "Fa_norm" else vec[1 + i]) for i, k in enumerate(keys)}
+        else:
+            loss_val = loss
+        names, data = ["loss"], [round(loss_val.cpu().item(), 3)]
         if losses.get("anneal", True):
             names.append("kl_w"); data.append(round(self.kl_w, 3))
-        for k, v in terms.items():
+        for k, v in shown.items():
             names.append(k)
-            data.append(round((norm if k == "Fa_norm" else v).cpu().item(), 3))
+            data.append(round(v.cpu().item(), 3))
         return loss, data, names
 
     def train_step(self, x, y, t, epoch, losses, eval_pts, grad_lim=300, n_samples=32, track_norms=False,
                    norm_file="grad_norms.txt"):
-        y_pred = self(x, t[eval_pts], n_samples=n_samples, training=True)
-        loss, data, names = self.calc_loss(y_pred, y[:, eval_pts, :], losses=losses)
-        loss.backward()
-        grad_norm = torch.norm(torch.cat([p.grad.reshape(-1) for p in self.parameters() if p.grad is not None]), 2).item()
+        if self._dp is not None and self._dp["world"] > 1:
+            B = x.shape[0]
+            lo, hi = self._shard(B)
+            self._dp_eps = (B, lo, hi)
+            try:
+                y_pred = self(x[lo:hi], t[eval_pts], n_samples=n_samples, training=True)
+            finally:
+                self._dp_eps = None
+            udist.sync_side_stats(self.ode, group=self._dp["group"])
+            self._dp_w = ((hi - lo) / B, 1.0 / self._dp["world"])
+            try:
+                loss, data, names = self.calc_loss(y_pred, y[lo:hi][:, eval_pts, :], losses=losses)
+            finally:
+                self._dp_w = None
+            loss.backward()
+            # one bucket: encoder + ODE + decoder gradients summed over the ranks (ref :205 then
+            # sees the global gradient on every rank: same gate, same Adam step)
+            udist.all_reduce_grads(self.parameters(), average=False, group=self._dp["group"])
+        else:
+            y_pred = self(x, t[eval_pts], n_samples=n_samples, training=True)
+            loss, data, names = self.calc_loss(y_pred, y[:, eval_pts, :], losses=losses)
+            loss.backward()
+        # every parameter must have a gradient (the reference's p.grad.data raises otherwise, :205)
+        grad_norm = torch.norm(torch.cat([p.grad.reshape(-1) for p in self.parameters()]), 2).item()
         self.batch_grad_norms.append(grad_norm)
         if grad_norm < grad_lim or self.skip_count >= 4 or epoch <= 3:
             self.optimizer.step()
@@ -251,7 +369,8 @@ class VAE:
                 y_pred = self(validate["x_test"], validate["t"], n_samples=validate["n_samples"], training=False)
                 y_pr, y_te = _scale_forecast(y_pred, validate["y_test"], validate["scaler"])
                 mu, sd = y_pr.mean(1), y_pr.std(1)
-                nlls = [Metrics.nll(y_te[:, g, :], mu[:, g, :], sd[:, g, :]) for g in range(len(validate["t"]))]
+                # the reference scores range(len(t)) with the TRAINING grid t (ref lib/VAE.py:278)
+                nlls = [Metrics.nll(y_te[:, g, :], mu[:, g, :], sd[:, g, :]) for g in range(len(t))]
                 self._history.epoch_history[-1]["forecast_nll"] = np.mean(nlls[-28:])
                 self._history.epoch_history[-1]["all_nll"] = np.mean(nlls)
             if disable:

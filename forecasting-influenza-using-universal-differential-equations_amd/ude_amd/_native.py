@@ -39,7 +39,9 @@ EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_
                     "ude_rk4_forward", "ude_rk4_backward", "ude_rk4_backward_sir", "ude_dopri5_workspace",
                     "ude_dopri5_forward", "ude_loss_head_workspace", "ude_loss_head_forward",
                     "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_rhs_workspace",
-                    "ude_rhs_forward", "ude_rhs_vjp", "ude_build_info")
+                    "ude_rhs_forward", "ude_rhs_vjp", "ude_pack_decoder", "ude_rk4_forward_dec",
+                    "ude_decoder_backward", "ude_nll_workspace", "ude_nll_forward", "ude_nll_backward",
+                    "ude_build_info")
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -62,7 +64,9 @@ class UdeSizes(ctypes.Structure):
     _fields_ = [("pack_bytes", ctypes.c_int64), ("sched_bytes", ctypes.c_int64), ("ckpt_bytes", ctypes.c_int64),
                 ("stats_slab_bytes", ctypes.c_int64), ("grad_slab_bytes", ctypes.c_int64),
                 ("n_params", ctypes.c_int64), ("grid_fwd", ctypes.c_int32), ("grid_bwd", ctypes.c_int32),
-                ("lds_fwd", ctypes.c_int32), ("lds_bwd", ctypes.c_int32)]
+                ("lds_fwd", ctypes.c_int32), ("lds_bwd", ctypes.c_int32),
+                ("dec_pack_bytes", ctypes.c_int64), ("ckpt_final_bytes", ctypes.c_int64),
+                ("dec_ws_bytes", ctypes.c_int64)]
 
 
 def make_desc(cfg: _cfgs.Config) -> UdeModelDesc:
@@ -135,6 +139,18 @@ class NativeLib:
         L.ude_rhs_forward.restype = i32
         L.ude_rhs_vjp.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ude_rhs_vjp.restype = i32
+        L.ude_pack_decoder.argtypes = [pdesc, vp, vp, vp, vp]
+        L.ude_pack_decoder.restype = i32
+        L.ude_rk4_forward_dec.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_rk4_forward_dec.restype = i32
+        L.ude_decoder_backward.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ude_decoder_backward.restype = i32
+        L.ude_nll_workspace.argtypes = [pdesc, i32, i32, i32, ctypes.POINTER(ctypes.c_int64)]
+        L.ude_nll_workspace.restype = i32
+        L.ude_nll_forward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp]
+        L.ude_nll_forward.restype = i32
+        L.ude_nll_backward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp]
+        L.ude_nll_backward.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -225,6 +241,33 @@ class NativeLib:
     def rhs_vjp(self, desc, prob, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, stream) -> None:
         check(self.lib.ude_rhs_vjp(ctypes.byref(desc), ctypes.byref(prob), pack, x, cot_f, cot_rates, cot_fa, dx,
                                    ws, dparams, stream), "ude_rhs_vjp")
+
+    def pack_decoder(self, desc, W, b, out, stream) -> None:
+        check(self.lib.ude_pack_decoder(ctypes.byref(desc), W, b, out, stream), "ude_pack_decoder")
+
+    def forward_dec(self, desc, prob, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, stats_out,
+                    reg_out, stream) -> None:
+        check(self.lib.ude_rk4_forward_dec(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, dec_pack, yhat,
+                                           ckpt, stats_slab, reg_slab, stats_out, reg_out, stream),
+              "ude_rk4_forward_dec")
+
+    def decoder_backward(self, desc, prob, sched, ckpt, dyhat, W, grad_reg, ws, dl3, dW, db, stream) -> None:
+        check(self.lib.ude_decoder_backward(ctypes.byref(desc), ctypes.byref(prob), sched, ckpt, dyhat, W, grad_reg,
+                                            ws, dl3, dW, db, stream), "ude_decoder_backward")
+
+    def nll_workspace(self, desc, T, S, B) -> int:
+        out = ctypes.c_int64(0)
+        check(self.lib.ude_nll_workspace(ctypes.byref(desc), int(T), int(S), int(B), ctypes.byref(out)),
+              "ude_nll_workspace")
+        return int(out.value)
+
+    def nll_forward(self, desc, T, S, B, yhat, y, ws, out, stream) -> None:
+        check(self.lib.ude_nll_forward(ctypes.byref(desc), int(T), int(S), int(B), yhat, y, ws, out, stream),
+              "ude_nll_forward")
+
+    def nll_backward(self, desc, T, S, B, yhat, y, grad, ws, dyhat, stream) -> None:
+        check(self.lib.ude_nll_backward(ctypes.byref(desc), int(T), int(S), int(B), yhat, y, grad, ws, dyhat,
+                                        stream), "ude_nll_backward")
 
     def build_info(self) -> str:
         return self.lib.ude_build_info().decode()

@@ -160,7 +160,9 @@ class _OdeintAdjoint(torch.autograd.Function):
                 aug_state[1] = y[i - 1]
                 aug_state[2] = aug_state[2] + grad_y[i - 1]
             if t_requires_grad:
-                time_vjps[0] = -aug_state[0]
+                # aug_state[0] already is dL/dt0: -sum_i g_i . f(t_i, y_i) carried back through the
+                # vjp_t dynamics (torchdiffeq: time_vjps[0] = aug_state[0], no negation)
+                time_vjps[0] = aug_state[0]
         try:
             func.last_adjoint_info = {"augmented_evals": counts["evals"], "seminorm": seminorm}
         except AttributeError:

@@ -21,34 +21,73 @@ import torch
 import torch.distributed as dist
 
 
+def _active(group=None) -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def world_size(group=None) -> int:
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def rank(group=None) -> int:
+    return dist.get_rank(group) if (dist.is_available() and dist.is_initialized()) else 0
+
+
 class _AllReduceSum(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, group):
+        ctx.group = group
         y = x.clone()
-        dist.all_reduce(y, op=dist.ReduceOp.SUM)
+        dist.all_reduce(y, op=dist.ReduceOp.SUM, group=group)
         return y
 
     @staticmethod
     def backward(ctx, g):
         g = g.clone()
-        dist.all_reduce(g, op=dist.ReduceOp.SUM)
-        return g
+        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
+        return g, None
 
 
-def all_reduce_sum(x: torch.Tensor) -> torch.Tensor:
+def all_reduce_sum(x: torch.Tensor, group=None) -> torch.Tensor:
     """Differentiable SUM all-reduce (identity when not distributed)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active(group):
         return x
-    return _AllReduceSum.apply(x)
+    return _AllReduceSum.apply(x, group)
 
 
-def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: torch.Tensor):
+def all_reduce_values(x: torch.Tensor, group=None) -> torch.Tensor:
+    """SUM all-reduce of a detached vector (reported loss terms)."""
+    if not _active(group):
+        return x
+    y = x.clone()
+    dist.all_reduce(y, op=dist.ReduceOp.SUM, group=group)
+    return y
+
+
+def broadcast_parameters(params: Iterable[torch.nn.Parameter], src: int = 0, group=None) -> None:
+    """Rank src's parameter values on every rank (one flat bucket)."""
+    if not _active(group):
+        return
+    ps = list(params)
+    if not ps:
+        return
+    with torch.no_grad():
+        flat = torch.cat([p.detach().reshape(-1) for p in ps])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        for p in ps:
+            n = p.numel()
+            p.copy_(flat[off:off + n].view_as(p))
+            off += n
+
+
+def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: torch.Tensor, group=None):
     """Global (n, mean, std, norm) from per-rank values (Chan's pooled variance, fp64)."""
     n = torch.tensor([n_local], dtype=torch.float64, device=mean.device)
     m = mean.double()
     s = std.double()
     suff = torch.cat([n, n * m, (n - 1.0) * s * s + n * m * m, norm.double().reshape(1) ** 2])
-    tot = all_reduce_sum(suff)
+    tot = all_reduce_sum(suff, group)
     n_tot = tot[0]
     gmean = tot[1:3] / n_tot
     gvar = (tot[3:5] - n_tot * gmean * gmean) / (n_tot - 1.0)
@@ -57,15 +96,17 @@ def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: t
     return n_tot, gmean.to(mean.dtype), gstd.to(std.dtype), gnorm.to(norm.dtype)
 
 
-def sync_side_stats(module) -> None:
+def sync_side_stats(module, group=None) -> None:
     """Replace the module's recorded fused-solve statistics by their global values."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _active(group):
         return
     # eager evaluations (params / tracker lists of per-evaluation tensors) are folded into
     # the same sufficient statistics as the fused solves' entries
+    from .rhs import eager_params
     groups = list(module._fused_rates)
-    if module.params:
-        p = torch.stack(module.params).reshape(-1, 2)
+    eager = eager_params(module.params)     # materialised fused entries are already in _fused_rates
+    if eager:
+        p = torch.stack(eager).reshape(-1, 2)
         groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
     tracker = list(module.tracker)
     if not groups and not tracker:
@@ -83,7 +124,7 @@ def sync_side_stats(module) -> None:
         norm = torch.norm(torch.cat([x.reshape(-1) for x in tracker])).reshape(1)
     else:
         norm = torch.zeros(1, device=m.device)
-    n_tot, gm, gs, gn = combine_stats(n, m, s, norm)
+    n_tot, gm, gs, gn = combine_stats(n, m, s, norm, group)
     module.params = []
     if groups:
         module._fused_rates = [(n_tot.detach(), gm, gs)]
@@ -91,17 +132,19 @@ def sync_side_stats(module) -> None:
         module.tracker = [gn]
 
 
-def all_reduce_grads(params: Iterable[torch.nn.Parameter], average: bool = True) -> None:
-    """One flat bucket (the ODE has <= ~0.3 MB of gradients: a single ring all-reduce)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+def all_reduce_grads(params: Iterable[torch.nn.Parameter], average: bool = True, group=None) -> None:
+    """One flat bucket (the ODE has <= ~0.3 MB of gradients, the whole VAE <= ~1 MB: a single
+    ring all-reduce).  Parameters without a gradient are skipped (the bucket layout is the same
+    on every rank: the same model, the same loss terms)."""
+    if not _active(group):
         return
     ps: List[torch.nn.Parameter] = [p for p in params if p.grad is not None]
     if not ps:
         return
     flat = torch.cat([p.grad.reshape(-1) for p in ps])
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     if average:
-        flat /= dist.get_world_size()
+        flat /= dist.get_world_size(group)
     off = 0
     for p in ps:
         n = p.grad.numel()

@@ -26,6 +26,10 @@ class Plan:
     n_times: int
     n_eval: int
     param_shapes: List[torch.Size]
+    # grid point of every output time when each one is an exact grid hit (decoder epilogue), else None
+    out_k: Optional[List[int]] = None
+    n_regions: int = 0
+    latent_dim: int = 0
 
 
 def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.device,
@@ -41,7 +45,12 @@ def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.d
     sizes = lib.query(desc, prob, dev_index)
     sched = torch.from_numpy(schedule.to_bytes()).to(device, non_blocking=False)
     n_eval = 4 * schedule.n_steps * n_traj * cfg[1]
-    return Plan(lib, desc, prob, sizes, sched, schedule.n_times, n_eval, param_shapes)
+    out_k = None
+    if schedule.n_steps >= 1 and all(int(m) == 1 for m in schedule.out_mode):
+        out_k = [0]
+        for n in range(schedule.n_steps):
+            out_k += [n + 1] * int(schedule.out_start[n + 1] - schedule.out_start[n])
+    return Plan(lib, desc, prob, sizes, sched, schedule.n_times, n_eval, param_shapes, out_k, cfg[1], cfg[2])
 
 
 # Optional HIP-event instrumentation (bench.py): when a list, every forward /
@@ -62,30 +71,16 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-class SirSink:
-    """Compact S, I, R cotangents of a fused solve's latent, deposited by consumers that read
-    only latent[..., :3] (the fused loss head, ude_amd/loss_head.py) in place of a full-size
-    (T, N, R, L) gradient that would be 5/8 zeros at L = 8.  A consumer that
-    deposits returns ZERO_GRAD-like stride-0 zeros for the latent itself, so the solve's backward
-    still runs; it adds the deposit to whatever full gradient other consumers produced."""
-
-    def __init__(self):
-        self.dl3 = None
-
-    def add(self, dl3: torch.Tensor) -> None:
-        self.dl3 = dl3 if self.dl3 is None else self.dl3 + dl3
-
-
 _ZEROS = {}
 
 
-def zero_grad_like(t: torch.Tensor) -> torch.Tensor:
-    """A stride-0 zero tensor of t's shape (no memory): the placeholder gradient of a latent
-    whose real cotangent went to its SirSink."""
-    key = (str(t.device), t.dtype)
+def zero_grad_like(t: torch.Tensor, device=None) -> torch.Tensor:
+    """A stride-0 zero tensor of t's shape (no memory), on t's device (or ``device``)."""
+    dev = torch.device(device) if device is not None else t.device
+    key = (str(dev), t.dtype)
     z = _ZEROS.get(key)
     if z is None:
-        z = _ZEROS[key] = torch.zeros((), dtype=t.dtype, device=t.device)
+        z = _ZEROS[key] = torch.zeros((), dtype=t.dtype, device=dev)
     return z.expand(t.shape)
 
 
@@ -94,10 +89,22 @@ def _is_placeholder(g: torch.Tensor) -> bool:
     return z is not None and g.data_ptr() == z.data_ptr() and all(st == 0 for st in g.stride())
 
 
+def sir_token_like(latent: torch.Tensor) -> torch.Tensor:
+    """Stride-0 (T, N, R, 3) placeholder output of a fused solve: a consumer that reads only
+    latent[..., :3] (the fused loss head) takes it as an input and returns its compact S, I, R
+    cotangent as the token's gradient, so the cotangent reaches the solve's backward through a
+    real autograd edge (correct under retain_graph / partial backward passes)."""
+    key = (str(latent.device), latent.dtype)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros((), dtype=latent.dtype, device=latent.device)
+    return z.expand(tuple(latent.shape[:3]) + (3,))
+
+
 class FusedRK4(torch.autograd.Function):
-    """Returns (latent, stats, ckpt); ckpt (the stage inputs of every step) is only a real
-    output when keep_ckpt is set (materialised tracking), else an empty tensor.  latent carries
-    a SirSink (``latent._ude_sir_sink``) for compact S, I, R cotangents."""
+    """Returns (latent, stats, ckpt, sir_token); ckpt (the stage inputs of every step) is only a
+    real output when keep_ckpt is set (materialised tracking), else an empty tensor; sir_token
+    (``sir_token_like``) receives compact S, I, R cotangents."""
 
     @staticmethod
     def forward(ctx, plan: Plan, y0: torch.Tensor, keep_ckpt: bool, *params: torch.Tensor):
@@ -121,24 +128,25 @@ class FusedRK4(torch.autograd.Function):
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
         ctx.plan = plan
-        ctx.sink = SirSink()
         ctx.set_materialize_grads(False)
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(out_ck)
-        latent._ude_sir_sink = ctx.sink
-        return latent, stats, out_ck
+        return latent, stats, out_ck, sir_token_like(latent)
 
     @staticmethod
-    def backward(ctx, dlatent, dstats, _dckpt=None):
+    def backward(ctx, dlatent, dstats, _dckpt=None, dl3=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats = ctx.saved_tensors
         dev = y0.device
         stream = _stream(dev)
-        dl3, ctx.sink.dl3 = ctx.sink.dl3, None
+        if dl3 is not None and _is_placeholder(dl3):
+            dl3 = None
+        if dl3 is not None:
+            dl3 = dl3.contiguous().to(torch.float32)
         if dlatent is not None and _is_placeholder(dlatent):
-            dlatent = None                          # every consumer deposited compactly
+            dlatent = None
         if dlatent is None and dl3 is None:
             dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         if dlatent is not None:
@@ -159,6 +167,121 @@ class FusedRK4(torch.autograd.Function):
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         return (None, dy0, None) + tuple(_split(dparams, plan.param_shapes))
+
+
+class FusedRK4Dec(torch.autograd.Function):
+    """Training solve with the decoder epilogue (lib/VAE.py:138, :186): the
+    forward kernel emits y_hat (T, N, R) = Decoder(latent[..., :3]) and reg =
+    latent_init_loss(latent[..., :3]) at the output times and writes no latent.  Returns
+    (y_hat, reg, stats, latent_token, ckpt): latent_token is a stride-0 (T, N, R, L) placeholder
+    (``materialize_latent`` turns it into the real latent on demand, its cotangent flowing back
+    through the token); ckpt is the training store the latent is rebuilt from.
+    Backward: ude_decoder_backward (d y_hat, d reg -> the compact S, I, R cotangent, d W_dec,
+    d b_dec, every output state read from the checkpoint) then ude_rk4_backward_sir."""
+
+    @staticmethod
+    def forward(ctx, plan: Plan, y0: torch.Tensor, Wd: torch.Tensor, bd: torch.Tensor, *params: torch.Tensor):
+        dev = y0.device
+        stream = _stream(dev)
+        sz = plan.sizes
+        ws = [p.contiguous() for p in params[0::2]]
+        bs = [p.contiguous() for p in params[1::2]]
+        Wd, bd = Wd.contiguous(), bd.contiguous()
+        pack = torch.empty(sz.pack_bytes // 4, dtype=torch.float32, device=dev)
+        plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
+        dec_pack = torch.empty(sz.dec_pack_bytes // 4, dtype=torch.float32, device=dev)
+        plan.lib.pack_decoder(plan.desc, Wd.data_ptr(), bd.data_ptr(), dec_pack.data_ptr(), stream)
+        N, R, L = y0.shape
+        yhat = torch.empty((plan.n_times, N, R), dtype=torch.float32, device=dev)
+        ckpt = torch.empty((sz.ckpt_bytes + sz.ckpt_final_bytes) // 4, dtype=torch.float32, device=dev)
+        stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
+        reg_slab = torch.empty(max(sz.grid_fwd, 1), dtype=torch.float64, device=dev)
+        stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        reg = torch.zeros(1, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
+        plan.lib.forward_dec(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                             dec_pack.data_ptr(), yhat.data_ptr(), ckpt.data_ptr(), stats_slab.data_ptr(),
+                             reg_slab.data_ptr(), stats.data_ptr(), reg.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("fwd_dec", e0, e1))
+        ctx.plan = plan
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(y0, pack, ckpt, stats, Wd)
+        ctx.mark_non_differentiable(ckpt)
+        token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
+        return yhat, reg[0], stats, token, ckpt
+
+    @staticmethod
+    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None):
+        plan: Plan = ctx.plan
+        y0, pack, ckpt, stats, Wd = ctx.saved_tensors
+        dev = y0.device
+        stream = _stream(dev)
+        sz = plan.sizes
+        N, R, L = y0.shape
+        T = plan.n_times
+        if dyhat is None or _is_placeholder(dyhat):
+            dyhat = torch.zeros((T, N, R), dtype=torch.float32, device=dev)
+        dyhat = dyhat.contiguous().to(torch.float32)
+        g_reg = torch.zeros(1, dtype=torch.float32, device=dev) if dreg is None else dreg.reshape(1).float()
+        dl3 = torch.empty((T, N, R, 3), dtype=torch.float32, device=dev)
+        dWd = torch.empty_like(Wd)
+        dbd = torch.empty(R, dtype=torch.float32, device=dev)
+        dec_ws = torch.empty(max(sz.dec_ws_bytes // 4, 1), dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
+        plan.lib.decoder_backward(plan.desc, plan.prob, plan.sched_dev.data_ptr(), ckpt.data_ptr(), dyhat.data_ptr(),
+                                  Wd.data_ptr(), g_reg.data_ptr(), dec_ws.data_ptr(), dl3.data_ptr(), dWd.data_ptr(),
+                                  dbd.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("dec_bwd", e0, e1))
+        full = None
+        if dlatent is not None and not _is_placeholder(dlatent):
+            # the materialised latent was used too: one full cotangent
+            full = dlatent.contiguous().to(torch.float32).clone()
+            full[..., :3] += dl3
+            dl3 = None
+        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+        dy0 = torch.empty_like(y0)
+        slab = torch.empty(max(sz.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
+        dparams = torch.empty(sz.n_params, dtype=torch.float32, device=dev)
+        if EVENTS is not None:
+            e0 = _ev(dev); e0.record()
+        plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                              ckpt.data_ptr(), _ptr(full), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
+                              dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        if EVENTS is not None:
+            e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
+        return (None, dy0, dWd, dbd) + tuple(_split(dparams, plan.param_shapes))
+
+
+class _LatentFromStore(torch.autograd.Function):
+    """The (T, N, R, L) latent of a decoder-epilogue solve, rebuilt on demand from its training
+    store (S, I, R of output j = the stage-0 checkpoint of grid point k_j, or the final-state
+    block) and y0's static dims; its cotangent goes back as the gradient of the solve's token."""
+
+    @staticmethod
+    def forward(ctx, token, ckpt, y0, plan: Plan):
+        N, R, L = y0.shape
+        n_tiles = (N + 15) // 16
+        n_steps = plan.prob.n_steps
+        F = 3 * R
+        dyn = ckpt[: n_tiles * n_steps * 4 * F * 16].view(n_tiles, n_steps, 4, F, 16)[:, :, 0]
+        off = plan.sizes.ckpt_bytes // 4
+        fin = ckpt[off: off + n_tiles * F * 16].view(n_tiles, 1, F, 16)
+        states = torch.cat([dyn, fin], 1)[:, plan.out_k]                    # (tiles, T, F, 16)
+        sir = states.permute(1, 0, 3, 2).reshape(len(plan.out_k), n_tiles * 16, R, 3)[:, :N]
+        static = y0[..., 3:].unsqueeze(0).expand(len(plan.out_k), N, R, L - 3)
+        return torch.cat([sir, static], -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None, None, None
+
+
+def materialize_latent(token: torch.Tensor, ckpt: torch.Tensor, y0: torch.Tensor, plan: Plan) -> torch.Tensor:
+    return _LatentFromStore.apply(token, ckpt, y0.detach(), plan)
 
 
 def _split(flat: torch.Tensor, shapes) -> List[torch.Tensor]:

@@ -21,7 +21,7 @@ from . import fused as _fused
 
 class _LossHead(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, lib, desc, T, S, B, latent, W, b, y):
+    def forward(ctx, lib, desc, T, S, B, latent, sir_token, W, b, y):
         dev = latent.device
         stream = _fused._stream(dev)
         dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -36,8 +36,9 @@ class _LossHead(torch.autograd.Function):
         if _fused.EVENTS is not None:
             e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_fwd", e0, e1))
         ctx.meta = (lib, desc, T, S, B)
-        # a latent straight from the fused solve takes its (S, I, R-only) cotangent compactly
-        ctx.sink = getattr(latent, "_ude_sir_sink", None) if COMPACT else None
+        # a latent straight from the fused solve takes its (S, I, R-only) cotangent compactly,
+        # as the gradient of the solve's sir_token output (fused.sir_token_like)
+        ctx.compact = sir_token is not None
         ctx.save_for_backward(latent, W, b, y, ws)
         ctx.mark_non_differentiable(ws)
         # ws starts with the per-(t, b, r) sample mean / std of the predictions ((T, B, R, 2))
@@ -48,10 +49,10 @@ class _LossHead(torch.autograd.Function):
         lib, desc, T, S, B = ctx.meta
         latent, W, b, y, ws = ctx.saved_tensors
         with torch.cuda.device(latent.device):
-            return _LossHead._backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, ctx.sink)
+            return _LossHead._backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, ctx.compact)
 
     @staticmethod
-    def _backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, sink):
+    def _backward(lib, desc, T, S, B, latent, W, b, y, ws, g_nll, g_reg, compact):
         dev = latent.device
         zero = torch.zeros((), dtype=torch.float32, device=dev)
         grad = torch.stack([zero if g_nll is None else g_nll.float().reshape(()),
@@ -60,14 +61,13 @@ class _LossHead(torch.autograd.Function):
         db = torch.empty_like(b)
         if _fused.EVENTS is not None:
             e0 = _fused._ev(dev); e0.record()
-        if sink is not None:
+        dl3 = dlat = None
+        if compact:
             N, R = latent.shape[1], latent.shape[2]
             dl3 = torch.empty((T, N, R, 3), dtype=torch.float32, device=dev)
             lib.loss_backward_sir(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
                                   grad.data_ptr(), ws.data_ptr(), dl3.data_ptr(), dW.data_ptr(), db.data_ptr(),
                                   _fused._stream(dev))
-            sink.add(dl3)
-            dlat = _fused.zero_grad_like(latent)
         else:
             dlat = torch.empty_like(latent)
             lib.loss_backward(desc, T, S, B, latent.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(),
@@ -75,11 +75,11 @@ class _LossHead(torch.autograd.Function):
                               _fused._stream(dev))
         if _fused.EVENTS is not None:
             e1 = _fused._ev(dev); e1.record(); _fused.EVENTS.append(("loss_bwd", e0, e1))
-        return None, None, None, None, None, dlat, dW, db, None
+        return None, None, None, None, None, dlat, dl3, dW, db, None
 
 
 _FITS = {}
-# hand the S, I, R cotangent to the fused solve's backward compactly (fused.SirSink) when the
+# hand the S, I, R cotangent to the fused solve's backward compactly (fused.sir_token_like) when the
 # latent comes straight from it; False: always write the full (T, N, R, L) d latent
 COMPACT = True
 
@@ -125,7 +125,8 @@ def fused_loss_head(ode, latent: torch.Tensor, linear: torch.nn.Linear, y: torch
     if tuple(y.shape) != (batch, T, ode.n_regions):
         raise ValueError(f"targets {tuple(y.shape)} do not match (B, T, R) = {(batch, T, ode.n_regions)}")
     with torch.cuda.device(latent.device):
-        nll, reg, ws = _LossHead.apply(lib, desc, T, int(n_samples), int(batch), latent, linear.weight,
+        token = getattr(latent, "_ude_sir_token", None) if COMPACT else None
+        nll, reg, ws = _LossHead.apply(lib, desc, T, int(n_samples), int(batch), latent, token, linear.weight,
                                        linear.bias, y.to(torch.float32))
     if group_stats:
         R = ode.n_regions

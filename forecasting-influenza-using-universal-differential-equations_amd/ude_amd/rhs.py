@@ -60,8 +60,21 @@ def _finish(flux3: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 class _FusedList(list):
     """Per-evaluation entries materialised from a fused solve (``materialize_tracking``): the
-    reference's list contents for readers; ``posterior()`` takes the same evaluations from the
-    solve's exact sufficient statistics instead, so they are not counted twice."""
+    reference's list contents for readers.  ``posterior()`` takes those evaluations from the
+    solve's exact sufficient statistics instead, so they are not counted twice; entries appended
+    by eager evaluations (evaluation kernel, autograd dopri5, euler ...) are not in ``fused_ids``
+    and are pooled as usual."""
+
+    def __init__(self, *args):
+        super().__init__(*args)
+        self.fused_ids = set()
+
+
+def eager_params(params) -> list:
+    """The entries of a ``params`` list that no fused solve's statistics already cover."""
+    if isinstance(params, _FusedList):
+        return [p for p in params if id(p) not in params.fused_ids]
+    return list(params)
 
 
 class _TrackerView(torch.autograd.Function):
@@ -117,7 +130,9 @@ class _UDEModule(nn.Module):
             if evals is not None:
                 if not isinstance(self.params, _FusedList):
                     self.params = _FusedList(self.params)
-                self.params.extend(evals[0].unbind(0))
+                entries = evals[0].unbind(0)
+                self.params.extend(entries)
+                self.params.fused_ids.update(id(e) for e in entries)
         if self.ode_type in ("Fa", "FaFp"):
             if evals is not None:
                 self.tracker.extend(_TrackerView.apply(stats, evals[1]).unbind(0))
@@ -152,8 +167,9 @@ class _UDEModule(nn.Module):
     def posterior(self) -> Normal:
         """Normal(mean, unbiased std) of every recorded rate; clears them (:152-156)."""
         groups = []
-        if self.params and not isinstance(self.params, _FusedList):
-            p = torch.stack(self.params).reshape(-1, 2)
+        eager = eager_params(self.params)
+        if eager:
+            p = torch.stack(eager).reshape(-1, 2)
             groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
         groups.extend(self._fused_rates)
         self.params = []

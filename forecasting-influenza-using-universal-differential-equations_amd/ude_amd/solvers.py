@@ -110,7 +110,8 @@ def _host_t(t: torch.Tensor) -> torch.Tensor:
     return host
 
 
-def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=None) -> torch.Tensor:
+def plan_for(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=None) -> "_fused.Plan":
+    """The cached launch plan (schedule on the device, buffer sizes) of a fused solve."""
     th = _host_t(t)
     if isinstance(step_size, torch.Tensor):
         step_size = step_size.detach().cpu()
@@ -118,35 +119,42 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         step_size.to(th.dtype).numpy().tobytes() if isinstance(step_size, torch.Tensor) else float(step_size))
     bayes = func.uncertainty == "bayes"
     if bayes:
-        mus, sds = func.ude_mean_std()
-        params = mus + sds
+        mus, _ = func.ude_mean_std()
+        shapes = [p.shape for p in mus]
     else:
-        params = []
-        for lin in func.ude_linears():
-            params += [lin.weight, lin.bias]
+        shapes = func.ude_weight_shapes()
     cfg = func.ude_config()
     fa_w = func.fa_weight()
     key = (cfg, str(th.dtype), th.numpy().tobytes(), step_key, int(y0.shape[0]), float(fa_w), str(y0.device),
-           tuple(tuple(p.shape) for p in params))
+           tuple(tuple(s) for s in shapes))
     plan = _PLAN_CACHE.get(key)
     if plan is None:
         sched = build_schedule(th, step_size)
-        shapes = [p.shape for p in (mus if bayes else params)]
-        plan = _fused.make_plan(cfg, sched, y0.shape[0], fa_w, y0.device, shapes)
+        plan = _fused.make_plan(cfg, sched, y0.shape[0], fa_w, y0.device, list(shapes))
         _lru_put(_PLAN_CACHE, key, plan)
     else:
         _PLAN_CACHE.move_to_end(key)
-    if bayes:
+    return plan
+
+
+def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=None) -> torch.Tensor:
+    plan = plan_for(func, y0, t, step_size)
+    if func.uncertainty == "bayes":
+        mus, sds = func.ude_mean_std()
         n_par = sum(int(p.numel()) for p in mus)
         eps = func.take_eps(4 * plan.prob.n_steps, n_par, y0.device)
         if func.materialize_tracking:
             raise NotImplementedError("materialize_tracking: Bayesian RHS (per-evaluation weight samples) "
                                       "is not supported")
-        latent, stats = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *params)
+        latent, stats = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *(mus + sds))
         func._record_fused(stats, plan.n_eval)
     else:
+        params = []
+        for lin in func.ude_linears():
+            params += [lin.weight, lin.bias]
         keep = bool(func.materialize_tracking)
-        latent, stats, ckpt = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
+        latent, stats, ckpt, sir_token = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
+        latent._ude_sir_token = sir_token
         evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps) if keep else None
         func._record_fused(stats, plan.n_eval, evals)
     return latent

@@ -77,6 +77,10 @@ typedef struct UdeSizes {
   int32_t grid_bwd;         /* workgroups launched by the backward               */
   int32_t lds_fwd;          /* bytes of LDS per workgroup                        */
   int32_t lds_bwd;
+  int64_t dec_pack_bytes;   /* packed decoder (ude_pack_decoder)                  */
+  int64_t ckpt_final_bytes; /* final-state block a decoder-epilogue training forward
+                               stores behind ckpt_bytes                          */
+  int64_t dec_ws_bytes;     /* ude_decoder_backward workspace                     */
 } UdeSizes;
 
 /*
@@ -221,6 +225,43 @@ int ude_rhs_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pac
 int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x, const float* cot_f,
                 const float* cot_rates, const float* cot_fa, float* dx, void* ws, float* dparams,
                 ude_stream_t stream);
+
+/* ---- decoder epilogue: the training solve without a latent ----------
+ * The VAE's training loss reads the latent only through y_pred = Decoder(latent[..., :3])
+ * (lib/models.py:27-51 Linear(3R -> R); lib/VAE.py:138) and latent_init_loss(latent[..., :3])
+ * (lib/train_functions.py:116-126, lib/VAE.py:186).  ude_rk4_forward_dec runs the training forward
+ * of ude_rk4_forward but emits, at every output time, y_hat (T, N, R) = W_dec . y[:3R] + b_dec
+ * (y_pred = y_hat.reshape(T, S, B, R).permute(2, 1, 0, 3)) and reg_out (device float) =
+ * latent_init_loss over every output's S, I, R, and writes no (T, N, R, L) latent.  Every output
+ * time must be a grid point (torchdiffeq exact hit: schedule mode 1) and n_steps >= 1.
+ *   dec_pack: ude_query's dec_pack_bytes, filled by ude_pack_decoder(W_dec (R, 3R), b_dec (R));
+ *   ckpt: ckpt_bytes + ckpt_final_bytes (the final state is stored behind the checkpoints);
+ *   stats_slab: stats_slab_bytes; reg_slab: grid_fwd doubles.
+ * ude_decoder_backward: given d y_hat (T, N, R) and grad_reg (device float, d loss / d reg_out)
+ * writes the compact S, I, R cotangent dl3 (T, N, R, 3) for ude_rk4_backward_sir (every output
+ * state read back from ckpt), d W_dec (R, 3R) and d b_dec (R); ws: dec_ws_bytes.
+ * ude_nll_*: nll_loss(y_pred, y) (lib/train_functions.py:81-90) over y_hat (T, S*B, R) with targets
+ * y (B, T, R), -1 = missing: out[0] = the mean nll; ws (ude_nll_workspace) keeps the per-group
+ * sample mean / std (T, B, R, 2) for the backward, which writes d y_hat given grad (device float,
+ * d loss / d nll). */
+int ude_pack_decoder(const UdeModelDesc* m, const float* W_dec, const float* b_dec, float* dec_pack,
+                     ude_stream_t stream);
+
+int ude_rk4_forward_dec(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                        const float* y0, const float* dec_pack, float* yhat, float* ckpt, double* stats_slab,
+                        double* reg_slab, float* stats_out, float* reg_out, ude_stream_t stream);
+
+int ude_decoder_backward(const UdeModelDesc* m, const UdeProblem* p, const void* sched, const float* ckpt,
+                         const float* dyhat, const float* W_dec, const float* grad_reg, void* ws, float* dl3,
+                         float* dW_dec, float* db_dec, ude_stream_t stream);
+
+int ude_nll_workspace(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, int64_t* ws_bytes);
+
+int ude_nll_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* yhat, const float* y,
+                    void* ws, float* out, ude_stream_t stream);
+
+int ude_nll_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* yhat, const float* y,
+                     const float* grad, const void* ws, float* dyhat, ude_stream_t stream);
 
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);

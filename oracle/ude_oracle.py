@@ -278,6 +278,111 @@ def solve_and_grad(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, step_size,
     return res
 
 
+def _chunk_stats(args):
+    """Pass 1 of ``solve_and_grad_chunked`` for one chunk: latent and fp64 side-statistic sums."""
+    rhs, y0c, t, step_size, threads = args
+    if threads:
+        torch.set_num_threads(threads)
+    with torch.no_grad():
+        rhs.clear_tracking()
+        lat = odeint_rk4(rhs, y0c, t, step_size)
+        out = {"latent": lat}
+        if rhs.params:
+            p = torch.stack(rhs.params).reshape(-1, 2).double()
+            out["n"], out["s1"], out["s2"] = p.shape[0], p.sum(0), p.pow(2).sum(0)
+        if rhs.tracker:
+            out["sf"] = float(torch.stack(rhs.tracker).double().pow(2).sum())
+    rhs.clear_tracking()
+    return out
+
+
+def _chunk_grad(args):
+    """Pass 2 of ``solve_and_grad_chunked`` for one chunk: gradient of its surrogate loss."""
+    rhs, y0c, t, step_size, dlc, dmean, dstd, dnorm, mean, std, norm, n, threads = args
+    if threads:
+        torch.set_num_threads(threads)
+    dt = y0c.dtype
+    ws = rhs.weights()
+    for w in ws:
+        w.requires_grad_(True)
+    yc = y0c.detach().clone().requires_grad_(True)
+    rhs.clear_tracking()
+    lat = odeint_rk4(rhs, yc, t, step_size)
+    loss = (lat * dlc.to(dt)).sum()
+    if mean is not None and dmean is not None:
+        p = torch.stack(rhs.params).reshape(-1, 2)
+        m, s = mean.to(dt), std.to(dt)
+        loss = loss + (p.sum(0) * dmean.to(dt) / n).sum() \
+            + ((p - m).pow(2).sum(0) * dstd.to(dt) / (2.0 * (n - 1) * s)).sum()
+    if norm is not None and dnorm is not None and float(norm) > 0:
+        loss = loss + dnorm * torch.stack(rhs.tracker).pow(2).sum() / (2.0 * norm.to(dt))
+    gr = torch.autograd.grad(loss, [yc] + ws, allow_unused=True)
+    rhs.clear_tracking()
+    for w in ws:
+        w.requires_grad_(False)
+    return [torch.zeros_like(v) if g is None else g.detach() for g, v in zip(gr, [yc] + ws)]
+
+
+def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, step_size,
+                           dlatent: torch.Tensor, dmean: Optional[torch.Tensor] = None,
+                           dstd: Optional[torch.Tensor] = None, dnorm: Optional[float] = None,
+                           chunk: int = 256, workers: int = 1) -> SolveResult:
+    """``solve_and_grad`` over trajectory chunks (bounded autograd memory for full-size batches),
+    optionally spread over ``workers`` spawned CPU processes (small-GEMM autograd does not use
+    many intra-op threads well).
+
+    Trajectories are independent; only the side statistics couple them, and their gradients are
+    linear in per-trajectory terms once the global values are known:
+      d mean / d p_i = 1/n,  d std / d p_i = (p_i - mean) / ((n-1) std),  d|Fa| / d Fa_i = Fa_i / |Fa|.
+    Pass 1 (no autograd) gives the global statistics (fp64 sums); pass 2 back-propagates each
+    chunk's surrogate  <lat_c, dl_c> + sum_i [dmean p_i / n + dstd (p_i - mean)^2 / (2 (n-1) std)]
+    + dnorm sum_i Fa_i^2 / (2 |Fa|)  (mean, std, |Fa| held constant), whose gradient equals the
+    chunk's share of the full loss gradient.  Weight gradients are summed over chunks in order.
+    """
+    N = y0.shape[0]
+    dt = y0.dtype
+    rhs.clear_tracking()
+    starts = list(range(0, N, chunk))
+    threads = max(1, torch.get_num_threads() // workers) if workers > 1 else 0
+
+    def run(fn, jobs):
+        if workers <= 1:
+            return [fn(j) for j in jobs]
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+            return list(ex.map(fn, jobs))
+
+    st = run(_chunk_stats, [(rhs, y0[c0:c0 + chunk], t, step_size, threads) for c0 in starts])
+    latent = torch.cat([s["latent"] for s in st], 1)
+    mean = std = norm = None
+    n = 0
+    if "s1" in st[0]:
+        n = sum(s["n"] for s in st)
+        s1 = sum(s["s1"] for s in st)
+        s2 = sum(s["s2"] for s in st)
+        mean = s1 / n
+        std = torch.sqrt(torch.clamp(s2 - n * mean * mean, min=0.0) / (n - 1))
+    if "sf" in st[0]:
+        norm = torch.tensor(math.sqrt(sum(s["sf"] for s in st)), dtype=torch.float64)
+    res = SolveResult(latent, None if mean is None else mean.to(dt), None if std is None else std.to(dt),
+                      None if norm is None else norm.to(dt))
+    gl = run(_chunk_grad, [(rhs, y0[c0:c0 + chunk], t, step_size, dlatent[:, c0:c0 + chunk], dmean, dstd, dnorm,
+                            mean, std, norm, n, threads) for c0 in starts])
+    names = ["y0"]
+    for i in range(len(rhs.p_w)):
+        names += [f"p_w{i}", f"p_b{i}"]
+    for i in range(len(rhs.a_w)):
+        names += [f"a_w{i}", f"a_b{i}"]
+    res.grads = {"y0": torch.cat([g[0] for g in gl], 0)}
+    for i, nm in enumerate(names[1:]):
+        acc = gl[0][1 + i]
+        for g in gl[1:]:
+            acc = acc + g[1 + i]
+        res.grads[nm] = acc
+    return res
+
+
 def normwise_rel(a: torch.Tensor, b: torch.Tensor) -> float:
     """||a - b|| / max(||b||, tiny), in fp64."""
     a = a.double()

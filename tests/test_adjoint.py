@@ -46,6 +46,25 @@ def test_adjoint_linear_ode_matches_matrix_exponential(pkg):
     assert normwise_rel(f.A.grad, Ar.grad) < 1e-7
 
 
+def test_adjoint_time_gradient_matches_analytic(pkg):
+    """dL/dt for L = sum_i c_i . y(t_i), y(t) = expm(A (t - t0)) y0: dL/dt_i = c_i . A y(t_i) for i >= 1
+    and dL/dt0 = -sum_{i>=1} c_i . A y(t_i) (torchdiffeq's time_vjps)."""
+    from torchdiffeq import odeint_adjoint
+    torch.manual_seed(3)
+    A = torch.randn(3, 3, dtype=torch.float64) * 0.5
+    y0 = torch.randn(4, 3, dtype=torch.float64)
+    t = torch.tensor([0.2, 0.7, 1.5], dtype=torch.float64).requires_grad_(True)
+    c = torch.randn(3, 4, 3, dtype=torch.float64)
+    ys = odeint_adjoint(_Linear(A), y0, t, rtol=1e-11, atol=1e-13, method="dopri5")
+    (ys * c).sum().backward()
+    with torch.no_grad():
+        yt = torch.stack([y0 @ torch.linalg.matrix_exp(A * float(tt - t[0])).T for tt in t])
+        dti = torch.stack([(c[i] * (yt[i] @ A.T)).sum() for i in range(3)])
+        want = dti.clone()
+        want[0] = -dti[1:].sum()
+    assert normwise_rel(t.grad, want) < 1e-8, (t.grad, want)
+
+
 def _uoracle(pkg, kind, R, dtype):
     torch.manual_seed(2)
     if kind == "FaFp":

@@ -17,9 +17,11 @@ WORLD = 2
 N = 96
 
 
-def _setup(pkg, dev):
+def _setup(pkg, dev, materialize=False):
     torch.manual_seed(0)
     mod = pkg.FaFp(10, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]).to(dev)
+    # materialised per-evaluation lists must not be counted twice by sync_side_stats
+    mod.materialize_tracking = materialize
     gen = torch.Generator().manual_seed(9)
     S = torch.rand(N, 10, generator=gen) * 0.4 + 0.5
     I = torch.rand(N, 10, generator=gen) * 0.05
@@ -42,7 +44,7 @@ def _loss(pkg, mod, y0, t, dl, world):
     return (lat * dl).sum() + stats_term / world, post.loc.detach(), post.scale.detach(), nrm.detach()
 
 
-def _worker(rank, port, q):
+def _worker(rank, port, q, materialize):
     try:
         sys.path.insert(0, REPO)
         pkg = import_pkg()
@@ -51,7 +53,7 @@ def _worker(rank, port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
         dev = torch.device("cuda", 0)
-        mod, y0, t, dl = _setup(pkg, dev)
+        mod, y0, t, dl = _setup(pkg, dev, materialize)
         lo, hi = (0, 40) if rank == 0 else (40, N)          # uneven shards
         loss, m, s, nrm = _loss(pkg, mod, y0[lo:hi].contiguous(), t, dl[:, lo:hi].contiguous(), WORLD)
         loss.backward()
@@ -64,18 +66,19 @@ def _worker(rank, port, q):
         q.put(("err", traceback.format_exc()))
 
 
-def test_two_rank_dp_matches_single_process(pkg):
+@pytest.mark.parametrize("materialize", [False, True], ids=["stats", "materialized"])
+def test_two_rank_dp_matches_single_process(pkg, materialize):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29600 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    port = 29600 + os.getpid() % 1000 + (7 if materialize else 0)
+    procs = [ctx.Process(target=_worker, args=(r, port, q, materialize)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(WORLD)]
     for p in procs:
         p.join(timeout=60)
     assert all(r[0] != "err" for r in res), [r[1] for r in res if r[0] == "err"]
-    mod, y0, t, dl = _setup(pkg, torch.device("cuda", 0))
+    mod, y0, t, dl = _setup(pkg, torch.device("cuda", 0), materialize)
     loss, m, s, nrm = _loss(pkg, mod, y0, t, dl, 1)
     loss.backward()
     ref = [p.grad.cpu() for p in mod.parameters()]

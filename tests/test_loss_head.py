@@ -127,15 +127,15 @@ def test_compact_sir_cotangent_matches_full(pkg, monkeypatch):
     cotangents (ude_loss_head_backward_sir -> ude_rk4_backward_sir) instead of a full
     (T, N, R, L) d latent that is 5/8 zeros.  Same step with the hand-off disabled: identical
     loss and bit-identical gradients (the compact path adds the same values in the same order)."""
-    from ude_amd import fused, loss_head
+    from ude_amd import _native, loss_head
     calls = []
-    real = fused.SirSink.add
-    monkeypatch.setattr(fused.SirSink, "add", lambda self, dl3: (calls.append(tuple(dl3.shape)), real(self, dl3)))
+    real = _native.NativeLib.loss_backward_sir
+    monkeypatch.setattr(_native.NativeLib, "loss_backward_sir",
+                        lambda self, *a: (calls.append("sir"), real(self, *a))[1])
     f1, loss_c, g_c = _vae_step(64, True, monkeypatch)
-    assert calls and calls[0][-1] == 3, calls
+    assert calls == ["sir"], calls
     calls.clear()
     monkeypatch.setattr(loss_head, "COMPACT", False)
-    monkeypatch.setattr(fused.SirSink, "add", lambda self, dl3: (calls.append(tuple(dl3.shape)), real(self, dl3)))
     f2, loss_f, g_f = _vae_step(64, True, monkeypatch)
     assert f1 and f2 and not calls
     assert torch.equal(loss_c, loss_f)
@@ -154,3 +154,37 @@ def test_compact_sir_cotangent_with_other_consumers(pkg, monkeypatch):
     assert f1 and f2 and torch.equal(loss_c, loss_f)
     for k in g_f:
         assert torch.equal(g_c[k], g_f[k]), (k, normwise_rel(g_c[k], g_f[k]))
+
+
+@pytest.mark.gpu
+def test_compact_sir_cotangent_retain_graph(pkg):
+    """A backward that reaches the loss head but not the solve (decoder grads only, retain_graph)
+    must not leak its S, I, R cotangent into a later backward through the solve: the compact
+    cotangent travels on an autograd edge (the solve's sir_token output), not in shared state."""
+    from ude_amd import loss_head
+    torch.manual_seed(0)
+    R, L, T, S, B = 1, 8, 5, 8, 4
+    ode = pkg.FaFp(R, latent_dim=L, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]).to(DEV)
+    dec = torch.nn.Linear(3 * R, R).to(DEV)
+    gen = torch.Generator().manual_seed(1)
+    Sv = torch.rand(S * B, R, generator=gen) * 0.4 + 0.5
+    Iv = torch.rand(S * B, R, generator=gen) * 0.05
+    y0 = torch.cat([Sv[..., None], Iv[..., None], (1 - Sv - Iv)[..., None], torch.randn(S * B, R, L - 3,
+                                                                                        generator=gen)], -1)
+    y0 = (y0 + 1e-5).to(DEV).requires_grad_(True)
+    y = torch.rand(B, T, R, generator=gen).to(DEV)
+    t = torch.arange(T, dtype=torch.float32).to(DEV)
+
+    def run():
+        ode.clear_tracking()
+        lat = pkg.odeint(ode, y0, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+        assert loss_head.eligible(ode, lat, dec, S, B)
+        nll, reg = loss_head.fused_loss_head(ode, lat, dec, y, S, B)
+        return nll + 0.1 * reg
+
+    loss = run()
+    g_ref = torch.autograd.grad(loss, [y0], retain_graph=True)[0]
+    loss2 = run()
+    torch.autograd.grad(loss2, [dec.weight], retain_graph=True)     # reaches the head only
+    g2 = torch.autograd.grad(loss2, [y0])[0]
+    assert torch.equal(g_ref, g2)

@@ -81,3 +81,24 @@ def test_materialized_lists_match_eager_solve(pkg, kind):
     _, _, _, _, g_s = _solve(pkg, mod, y0, t, False)
     for k in g_s:
         assert normwise_rel(g_f[k], g_s[k]) < 1e-5, k
+
+
+@pytest.mark.gpu
+def test_materialized_then_eager_evaluation_pooled(pkg):
+    """A fused solve with materialised lists followed by a direct evaluation of the module
+    (evaluation kernel): posterior() pools both -- the materialised entries once (from the
+    solve's statistics), the eager entry as well (not dropped)."""
+    mod, y0, t = _case(pkg, "Fp", "cuda")
+    mod_c, y0_c, _ = _case(pkg, "Fp", "cpu")
+    mod_c.load_state_dict({k: v.cpu() for k, v in mod.state_dict().items()})
+    posts = []
+    for m, y, mat in ((mod, y0, True), (mod_c, y0_c, False)):
+        m.materialize_tracking = mat
+        m.clear_tracking()
+        with torch.no_grad():
+            pkg.odeint(m, y.detach(), t, method="rk4", options=dict(step_size=t[1] - t[0]))
+            m(t[0], y.detach() * 0.9)                 # one more evaluation, appended eagerly
+        assert len(m.params) == 4 * (len(t) - 1) + 1
+        posts.append(m.posterior())
+    assert normwise_rel(posts[0].loc, posts[1].loc) < 1e-5
+    assert normwise_rel(posts[0].scale, posts[1].scale) < 1e-5

@@ -1,0 +1,121 @@
+"""Data-parallel VAE training step (BASELINE configs[4]) through the reference API.
+
+``VAE.train_step`` under a 2-rank process group (gloo) shards the batch's windows, makes the
+posterior / |Fa| statistics global before ``calc_loss``, weights every loss term by its share
+of the global loss and all-reduces the encoder + ODE + decoder gradients in one bucket before
+the grad-norm gate.  Checked against the single-process ``train_step`` on the same batch
+(tests/golden/e2e_vae_us.npz inputs, eps replayed): global loss to 1e-6 relative, every
+gradient to 1e-5 normwise, identical parameters after the Adam step on both ranks.
+CPU: eager solver; GPU: both ranks on cuda:0 (the 1-GPU box) running the fused kernels."""
+import os
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import REPO, import_pkg, load_golden
+
+WORLD = 2
+
+
+def _model(g, device):
+    import lib.VAE as vae_mod
+    import lib.models as models
+    m = g["meta"]
+    model = vae_mod.VAE(models.Encoder_Back_GRU, models.FaFp, models.Decoder, m["n_qs"], 8, m.get("n_regions", 1),
+                        ode_params=dict(m["ode_params"], prior_std=0.05), enc_params=m["enc_params"],
+                        uncertainty=True, ode_kl_w=1 / 153)
+    for part in ("enc", "ode", "dec"):
+        mod = getattr(model, part)
+        sd = {k[len(part) + 3:]: torch.from_numpy(g[k]) for k in g if k.startswith(f"w_{part}.")}
+        mod.load_state_dict(sd, strict=True)
+    model.to(device)
+    model.setup_training(lr=1e-3)
+    return model
+
+
+def _step(model, g, device):
+    """One train_step; returns (global loss, {param name: grad}, {param name: value after step})."""
+    eps = torch.from_numpy(g["eps"]).to(device)
+    real_randn = torch.randn
+    torch.randn = lambda *a, **k: eps.clone()
+    captured = {}
+    real_calc = model.calc_loss
+
+    def calc(*a, **k):
+        loss, data, names = real_calc(*a, **k)
+        captured["loss"] = loss
+        return loss, data, names
+    model.calc_loss = calc
+    try:
+        x = torch.from_numpy(g["x"]).to(device)
+        y = torch.from_numpy(g["y"]).to(device)
+        t = torch.from_numpy(g["t"])
+        model.train_step(x, y, t, epoch=0, losses=g["meta"]["losses"], eval_pts=g["eval_pts"],
+                         n_samples=int(g["meta"]["n_samples"]))
+    finally:
+        torch.randn = real_randn
+        model.calc_loss = real_calc
+    loss = captured["loss"].detach().double().reshape(1)
+    from ude_amd import distributed as udist
+    loss = udist.all_reduce_values(loss)
+    named = [(f"{part}.{k}", p) for part in ("enc", "ode", "dec") for k, p in getattr(model, part).named_parameters()]
+    return (float(loss), {n: p.grad.detach().cpu().clone() for n, p in named},
+            {n: p.detach().cpu().clone() for n, p in named})
+
+
+def _worker(rank, port, q, device):
+    try:
+        sys.path.insert(0, REPO)
+        import_pkg()
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        g = load_golden("e2e_vae_us")
+        model = _model(g, device)
+        assert model._dp is not None and model._dp["world"] == WORLD
+        loss, grads, after = _step(model, g, device)
+        # numpy over the queue (torch tensors would be shared-memory handles of an exited process)
+        q.put((rank, loss, {k: v.numpy() for k, v in grads.items()}, {k: v.numpy() for k, v in after.items()}))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def _run(device, port_off):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 28500 + os.getpid() % 1000 + port_off
+    procs = [ctx.Process(target=_worker, args=(r, port, q, device)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] != "err" for r in res), [r[1] for r in res if r[0] == "err"]
+    g = load_golden("e2e_vae_us")
+    ref_loss, ref_grads, ref_after = _step(_model(g, device), g, device)
+    res = [(r, l, {k: torch.from_numpy(v) for k, v in gr.items()}, {k: torch.from_numpy(v) for k, v in af.items()})
+           for r, l, gr, af in res]
+    for rank, loss, grads, after in res:
+        assert abs(loss - ref_loss) <= 1e-6 * abs(ref_loss), (rank, loss, ref_loss)
+        for k in ref_grads:
+            a, b = grads[k].double(), ref_grads[k].double()
+            err = float((a - b).norm() / max(float(b.norm()), 1e-30))
+            assert err < 1e-5, (rank, k, err)
+    # identical Adam step on every rank
+    (_, _, _, a0), (_, _, _, a1) = res
+    for k in a0:
+        assert torch.equal(a0[k], a1[k]), k
+
+
+def test_vae_dp_step_matches_single_process_cpu(pkg):
+    _run("cpu", 0)
+
+
+@pytest.mark.gpu
+def test_vae_dp_step_matches_single_process_gpu(pkg):
+    _run("cuda", 11)

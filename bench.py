@@ -45,6 +45,9 @@ WORKLOADS = {
     "state49_n2048": dict(_STATE, n_traj=2048, t=("arange", 9, 1.0),
                           desc="state model R=49 (joint), the reference's own batch: 64 MC samples x 32 windows, "
                                "8 weekly RK4 steps (SURVEY 8d M2 variant)"),
+    "state49_n2560": dict(_STATE, n_traj=2560, t=("arange", 9, 1.0),
+                          desc="state model R=49 (joint), 2,560 trajectories = the per-GPU shard of the 20,480 "
+                               "batch strong-scaled over 8 MI355X (BASELINE configs[4]), 8 weekly RK4 steps"),
     "m3_states_r1": dict(_US, n_traj=64 * 50 * 10 * 32, t=("arange", 9, 1.0),
                          desc="50 independent states as R=1 US-architecture models: 64 samples x 50 states x "
                               "10 seasons x 32 windows = 1,024,000 trajectories, 8 weekly RK4 steps (SURVEY 8d M3)"),
@@ -325,42 +328,61 @@ def bayes_large_line(pkg, dev, steps=3):
 
 
 def train_head_line(pkg, w, dev, reps=10):
-    """one training step of the state49 workload through the fused solve and
-    the fused loss head (decoder + nll_loss + latent_init_loss), backward into the solve: with
-    the S, I, R-only cotangent hand-off (no full-size d latent written or read) vs without."""
+    """one training step of the state49 workload (64 MC samples x 320 windows,
+    9 weekly outputs) through the loss terms that read the latent -- y_pred = Decoder(latent[..., :3]),
+    nll_loss, 0.1 latent_init_loss -- plus the posterior / |Fa| terms, backward into the solve:
+    (a) the decoder epilogue (ude_rk4_forward_dec: y_hat and reg from the forward kernel, no latent
+    written; nll kernels; decoder backward from the checkpoint store), the path lib/VAE.py takes;
+    (b) the solve writing the latent + the fused loss head over it (the r02 path)."""
     import lib.models as models
-    from ude_amd import loss_head
+    from ude_amd import decoder_head, fused, loss_head
     mod, y0, t, _ = build(pkg, w, dev, seed=31)
     S, B, R = 64, w["n_traj"] // 64, w["R"]
     dec = models.Decoder(R, w["L"], 1).to(dev)
     y = torch.rand(B, len(t), R, device=dev, generator=torch.Generator(device=dev).manual_seed(4))
     lin = dec.decoder[-1]
+    h = t[1] - t[0]
 
-    def step():
+    def stats_terms():
+        post = mod.posterior()
+        return post.loc.sum() + post.scale.sum() + 0.1 * torch.norm(torch.stack(mod.tracker))
+
+    def step_epilogue():
         mod.clear_tracking()
         mod.zero_grad(set_to_none=True)
         y0.grad = None
-        lat = pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+        yhat, reg, lazy, _ = decoder_head.solve_decode(mod, y0, t, h, lin)
+        nll, _ = decoder_head.nll_head(mod, yhat, y, S, B)
+        (nll + 0.1 * reg + stats_terms()).backward()
+
+    def step_latent():
+        mod.clear_tracking()
+        mod.zero_grad(set_to_none=True)
+        y0.grad = None
+        lat = pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=h))
         nll, reg = loss_head.fused_loss_head(mod, lat, lin, y, S, B)
-        post = mod.posterior()
-        loss = nll + 0.1 * reg + post.loc.sum() + post.scale.sum() + 0.1 * torch.norm(torch.stack(mod.tracker))
-        loss.backward()
+        (nll + 0.1 * reg + stats_terms()).backward()
 
     out = {}
-    for compact in (True, False):
-        loss_head.COMPACT = compact
+    for name, fn in (("decoder_epilogue", step_epilogue), ("latent_loss_head", step_latent)):
         for _ in range(3):
-            step()
+            fn()
         torch.cuda.synchronize()
+        fused.EVENTS = []
         t0 = time.perf_counter()
         for _ in range(reps):
-            step()
+            fn()
         torch.cuda.synchronize()
-        out["ms_per_step_sir_handoff" if compact else "ms_per_step_full_dlatent"] = (time.perf_counter() - t0) / reps * 1e3
-    loss_head.COMPACT = True
+        out["ms_per_step_" + name] = (time.perf_counter() - t0) / reps * 1e3
+        k = {}
+        for kind, e0, e1 in fused.EVENTS:
+            k.setdefault(kind, []).append(e0.elapsed_time(e1))
+        fused.EVENTS = None
+        out["kernel_ms_" + name] = {kk: sum(v) / len(v) for kk, v in k.items()}
     n = w["n_traj"] * len(t) * R
-    return dict(workload="state49 training step: fused RK4 solve + fused loss head, fwd+bwd", **out,
-                dlatent_bytes_full=n * w["L"] * 4, dlatent_bytes_sir=n * 3 * 4)
+    return dict(workload="state49 training step: fused RK4 solve + decoder / nll_loss / latent_init_loss + "
+                         "posterior / |Fa| terms, fwd+bwd", **out,
+                latent_bytes_not_written=n * w["L"] * 4, yhat_bytes=n * 4)
 
 
 def _cpu_copy(mod):
@@ -369,14 +391,21 @@ def _cpu_copy(mod):
     return copy.deepcopy(mod).cpu()
 
 
+PMC_SOURCE = {}
+
+
 def read_pmc(name):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None)."""
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (or None).  rocprofv3 cannot
+    collect counters inside this process, so the value comes from the committed profile; the
+    profile's file and the commit it was measured at go into roofline.traffic_source."""
     p = os.path.join(REPO, "profiles", "pmc_" + name + ".json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
             d = json.load(f)
+        PMC_SOURCE[name] = {"file": os.path.relpath(p, REPO), "measured_at_commit": d.get("commit"),
+                            "kernel_avg_ms": d.get("kernel_avg_ms")}
         return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
@@ -520,7 +549,8 @@ def main():
             "roofline": {"kernel": "ude_bwd_kernel (+ grad finalize)", "bound": "mfma",
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
-                         "traffic": pmc, "avg_launch_ms": kms["bwd"],
+                         "traffic": pmc, "traffic_source": PMC_SOURCE.get(args.workload + "_bwd"),
+                         "avg_launch_ms": kms["bwd"],
                          "algorithmic_flop_per_launch": bwd_flop_launch},
             "kernels": {"fwd_ms": kms["fwd"], "bwd_ms": kms["bwd"],
                         "fwd_tflops": fwd_flop_launch / (kms["fwd"] * 1e-3) / 1e12 if kms["fwd"] else None,
@@ -535,6 +565,8 @@ def main():
                                                 target_rhs_evals_per_s=1e7)),
                  ("north_star_M1_fp32", lambda: extra_line(pkg, udist, "us_fp32", dev, barrier)),
                  ("M2_state49_n2048", lambda: extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=10)),
+                 ("state49_n2560_strong8_shard", lambda: extra_line(pkg, udist, "state49_n2560", dev, barrier,
+                                                                    steps=10)),
                  ("M3_states_r1", lambda: extra_line(pkg, udist, "m3_states_r1", dev, barrier)),
                  ("bayes_M1", lambda: extra_line(pkg, udist, "bayes_us", dev, barrier)),
                  ("dopri5_state49", lambda: dopri5_line(pkg, w, dev)),
@@ -550,6 +582,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.rehearse_cpu:
         res["cpu_baseline"] = cpu_baseline(w, mod, threads=CPU_THREADS)
         res["cpu_baseline_1thread"] = cpu_baseline(w, mod, threads=1)
+        if (os.cpu_count() or 1) > CPU_THREADS:
+            # also at every visible host core (more than this box's share per GPU)
+            res["cpu_baseline_all_visible_cores"] = cpu_baseline(w, mod, threads=os.cpu_count())
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

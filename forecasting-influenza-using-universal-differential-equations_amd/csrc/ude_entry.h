@@ -90,7 +90,14 @@ struct Ops {
   // BAYES: one weight sample per RHS evaluation (4 per RK4 step)
   static int64_t n_evals(const UdeProblem* p) { return M::BAYES ? 4 * (int64_t)p->n_steps : 1; }
 
+  // UdeProblem.recompute: the Recompute<M> view of the model (no stored activations)
+  static constexpr bool RC_VIEW = M::ACT_STORED;
+  static bool rc(const UdeProblem* p) { return RC_VIEW && p->recompute; }
+
   static int query(const UdeProblem* p, int device, UdeSizes* o) {
+    if constexpr (RC_VIEW) {
+      if (p->recompute) return Ops<Recompute<M>>::query(p, device, o);
+    }
     if (p->n_traj < 1 || p->n_steps < 0 || p->n_out < 0) return UDE_E_INVALID;
     if (M::BAYES && 4 * (int64_t)p->n_steps > 65535) return UDE_E_INVALID;   // grid.y / grid.z of the packers
     const int n_tiles = (p->n_traj + TT - 1) / TT;
@@ -117,6 +124,7 @@ struct Ops {
     o->dec_pack_bytes = (int64_t)M::DEC_PACK * 4;
     o->ckpt_final_bytes = (int64_t)n_tiles * M::F * TT * 4;
     o->dec_ws_bytes = (int64_t)gd * LossDims<M::R>::SLAB * 4;
+    o->act_bytes = M::ACT_STORED ? (int64_t)n_tiles * p->n_steps * 4 * TT * M::ACT_A4 * 4 : 0;
     return UDE_OK;
   }
 
@@ -146,6 +154,11 @@ struct Ops {
   static int forward_dec(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
                          const float* dec_pack, float* yhat, float* ckpt, double* stats_slab, double* reg_slab,
                          float* stats_out, float* reg_out, hipStream_t s) {
+    if constexpr (RC_VIEW) {
+      if (p->recompute)
+        return Ops<Recompute<M>>::forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab,
+                                              stats_out, reg_out, s);
+    }
     if (M::BAYES) return UDE_E_UNSUPPORTED;
     if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !stats_out || !reg_out)
       return UDE_E_INVALID;
@@ -182,6 +195,9 @@ struct Ops {
   static int dec_backward(const UdeProblem* p, const void* sched, const float* ckpt, const float* dyhat,
                           const float* W, const float* grad_reg, void* ws, float* dl3, float* dW, float* db,
                           hipStream_t s) {
+    if constexpr (RC_VIEW) {
+      if (p->recompute) return Ops<Recompute<M>>::dec_backward(p, sched, ckpt, dyhat, W, grad_reg, ws, dl3, dW, db, s);
+    }
     if (!sched || !ckpt || !dyhat || !W || !grad_reg || !ws || !dl3 || !dW || !db) return UDE_E_INVALID;
     if (p->n_steps < 1) return UDE_E_INVALID;
     int dev = 0;
@@ -291,6 +307,10 @@ struct Ops {
 
   static int forward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
                      float* latent, float* ckpt, double* stats_slab, float* stats_out, hipStream_t s) {
+    if constexpr (RC_VIEW) {
+      if (p->recompute && ckpt) return Ops<Recompute<M>>::forward(p, pack, sched, y0, latent, ckpt, stats_slab,
+                                                                  stats_out, s);
+    }
     if (!pack || !sched || !y0 || !latent || !stats_slab || !stats_out) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -320,6 +340,10 @@ struct Ops {
   static int backward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
                       const float* ckpt, const float* dlatent, const float* dlat_sir, const float* stats_out,
                       const float* dstats, float* dy0, float* slab, float* dparams, hipStream_t s) {
+    if constexpr (RC_VIEW) {
+      if (p->recompute) return Ops<Recompute<M>>::backward(p, pack, sched, y0, ckpt, dlatent, dlat_sir, stats_out,
+                                                           dstats, dy0, slab, dparams, s);
+    }
     if (!pack || !sched || !y0 || !stats_out || !dstats || !dy0 || !slab || !dparams) return UDE_E_INVALID;
     if (p->n_steps > 0 && !ckpt) return UDE_E_INVALID;
     int dev = 0;

@@ -369,4 +369,17 @@ struct Model {
   static constexpr int LDS_F_DEC = LDS_F + NTHREADS * 8;
 };
 
+// The same model without stored activations (memory fallback, UdeProblem.recompute): the training
+// forward stores only the 3R stage inputs per stage and the backward re-runs each stage's layer
+// phases from them (long-horizon row) -- O(steps * 3R) floats per trajectory instead of
+// O(steps * activations).  Every kernel reads these through M::, so the derived names win.
+template <class B>
+struct Recompute : B {
+  static constexpr bool STORE_ACT = false, STORE_ACT_D = false, ACT_STORED = false;
+  static constexpr bool SPLIT_BWD = false, SPLIT_FWD = false;
+  static constexpr int BWD_THREADS = NTHREADS;
+  static constexpr int LDS_B = B::ACT_STG * 4;
+  static constexpr int LDS_F_DEC = B::LDS_F + NTHREADS * 8;
+};
+
 }  // namespace ude

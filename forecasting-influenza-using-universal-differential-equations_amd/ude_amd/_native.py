@@ -52,7 +52,7 @@ class UdeModelDesc(ctypes.Structure):
 
 class UdeProblem(ctypes.Structure):
     _fields_ = [("n_traj", ctypes.c_int32), ("n_steps", ctypes.c_int32), ("n_out", ctypes.c_int32),
-                ("fa_w", ctypes.c_float)]
+                ("fa_w", ctypes.c_float), ("recompute", ctypes.c_int32)]
 
 
 class UdeDopriInfo(ctypes.Structure):
@@ -66,7 +66,7 @@ class UdeSizes(ctypes.Structure):
                 ("n_params", ctypes.c_int64), ("grid_fwd", ctypes.c_int32), ("grid_bwd", ctypes.c_int32),
                 ("lds_fwd", ctypes.c_int32), ("lds_bwd", ctypes.c_int32),
                 ("dec_pack_bytes", ctypes.c_int64), ("ckpt_final_bytes", ctypes.c_int64),
-                ("dec_ws_bytes", ctypes.c_int64)]
+                ("dec_ws_bytes", ctypes.c_int64), ("act_bytes", ctypes.c_int64)]
 
 
 def make_desc(cfg: _cfgs.Config) -> UdeModelDesc:

@@ -32,6 +32,23 @@ class Plan:
     latent_dim: int = 0
 
 
+# Stored-activation budget (bytes) of one training solve: above it the training forward stores only
+# the stage inputs and the backward recomputes each stage's layers (UdeProblem.recompute; same
+# results bit for bit).  None: half of the device's free memory when the plan is made.
+ACT_BUDGET = None
+
+
+def act_budget(device: torch.device) -> int:
+    import os
+    env = os.environ.get("UDE_ACT_BUDGET_BYTES")
+    if env is not None:
+        return int(float(env))
+    if ACT_BUDGET is not None:
+        return int(ACT_BUDGET)
+    free, _ = torch.cuda.mem_get_info(device)
+    return free // 2
+
+
 def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.device,
               param_shapes: List[torch.Size]) -> Plan:
     lib = _native.library_for(cfg)
@@ -41,8 +58,12 @@ def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.d
     prob.n_steps = schedule.n_steps
     prob.n_out = schedule.n_out
     prob.fa_w = float(fa_w)
+    prob.recompute = 0
     dev_index = device.index if device.index is not None else torch.cuda.current_device()
     sizes = lib.query(desc, prob, dev_index)
+    if sizes.act_bytes > 0 and sizes.act_bytes > act_budget(device):
+        prob.recompute = 1                      # memory fallback: recompute each stage's layers
+        sizes = lib.query(desc, prob, dev_index)
     sched = torch.from_numpy(schedule.to_bytes()).to(device, non_blocking=False)
     n_eval = 4 * schedule.n_steps * n_traj * cfg[1]
     out_k = None

@@ -63,6 +63,11 @@ typedef struct UdeProblem {
   int32_t n_steps;
   int32_t n_out;
   float fa_w;            /* FaFp.Fa_w (lib/models.py:225)                */
+  int32_t recompute;     /* 0: the training forward stores every stage's activation rows
+                            (UdeSizes.act_bytes of the checkpoint) and the backward reads
+                            them; 1: memory fallback -- only the 3R stage inputs are stored
+                            and the backward re-runs each stage's layers from them (same
+                            results, bit for bit).  Forward and backward must agree. */
 } UdeProblem;
 
 /* Buffer sizes in bytes for one (model, problem). */
@@ -81,6 +86,8 @@ typedef struct UdeSizes {
   int64_t ckpt_final_bytes; /* final-state block a decoder-epilogue training forward
                                stores behind ckpt_bytes                          */
   int64_t dec_ws_bytes;     /* ude_decoder_backward workspace                     */
+  int64_t act_bytes;        /* part of ckpt_bytes holding stored activation rows
+                               (0 with UdeProblem.recompute = 1)                 */
 } UdeSizes;
 
 /*

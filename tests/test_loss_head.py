@@ -69,10 +69,12 @@ def test_loss_head_rejects_oversized_sample_tile(pkg):
     assert not loss_head.eligible(ode, lat[..., 1:], lin, S, B)              # not the model's L
 
 
-def _vae_step(S, fused_ok, monkeypatch, mse=False):
+def _vae_step(S, fused_ok, monkeypatch, mse=False, epilogue=False):
+    """One VAE calc_loss + backward.  fused_ok: the fused loss head over a written latent may run;
+    epilogue: the decoder-epilogue solve (y_hat from the forward kernel, no latent) may run."""
     import lib.VAE as vae_mod
     import lib.models as models
-    from ude_amd import loss_head
+    from ude_amd import decoder_head, loss_head
     torch.manual_seed(3)
     model = vae_mod.VAE(models.Encoder_Back_GRU, models.FaFp, models.Decoder, 4, 8, 1,
                         ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
@@ -86,6 +88,8 @@ def _vae_step(S, fused_ok, monkeypatch, mse=False):
     eps = torch.randn(S, 3, 1, 7, generator=gen).to(DEV)
     if not fused_ok:
         monkeypatch.setattr(loss_head, "eligible", lambda *a, **k: False)
+    if not epilogue:
+        monkeypatch.setattr(decoder_head, "eligible", lambda *a, **k: False)
     real_randn = torch.randn
     monkeypatch.setattr(torch, "randn", lambda *a, **k: eps.clone())
     y_pred = model(x, t, n_samples=S, training=True)
@@ -112,6 +116,52 @@ def test_vae_calc_loss_fused_head_matches_eager(pkg, monkeypatch):
     assert normwise_rel(loss_f, loss_e) < 1e-5
     for k in g_e:
         assert normwise_rel(g_f[k], g_e[k]) < 5e-5, (k, normwise_rel(g_f[k], g_e[k]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mse", [False, True], ids=["nll_reg", "with_mse"])
+def test_vae_calc_loss_decoder_epilogue_matches_eager(pkg, monkeypatch, mse):
+    """the training step with the decoder epilogue (y_hat + latent_init_loss from the
+    solve's forward kernel, no latent written; nll kernels; decoder backward from the checkpoint
+    store) against the reference's own ops over a written latent: loss to 1e-5, every gradient to
+    5e-5; with mse the prediction also feeds torch ops (d y_hat from two consumers)."""
+    f_on, loss_f, g_f = _vae_step(64, False, monkeypatch, mse=mse, epilogue=True)
+    f_off, loss_e, g_e = _vae_step(64, False, monkeypatch, mse=mse)
+    assert f_on and not f_off
+    assert normwise_rel(loss_f, loss_e) < 1e-5
+    for k in g_e:
+        assert normwise_rel(g_f[k], g_e[k]) < 5e-5, (k, normwise_rel(g_f[k], g_e[k]))
+
+
+@pytest.mark.gpu
+def test_decoder_epilogue_latent_materialised_on_read(pkg):
+    """VAE.latent after a decoder-epilogue training call is rebuilt from the training store on
+    first read: equal to the latent a plain solve writes, and differentiable (its cotangent
+    reaches y0 / the weights through the solve's backward)."""
+    import lib.VAE as vae_mod
+    import lib.models as models
+    from ude_amd.decoder_head import LazyLatent
+    torch.manual_seed(3)
+    model = vae_mod.VAE(models.Encoder_Back_GRU, models.FaFp, models.Decoder, 4, 8, 1,
+                        ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
+                        enc_params={"q_sizes": [16, 8], "ff_sizes": [8], "SIR_scaler": [0.1, 0.05, 1.0]})
+    model.to(DEV)
+    model.setup_training()
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(3, 6, 5, generator=gen).to(DEV)
+    t = torch.arange(4, dtype=torch.float32)
+    model(x, t, n_samples=8, training=True)
+    lazy = model.__dict__["_latent"]
+    assert isinstance(lazy, LazyLatent) and not lazy.materialized
+    lat = model.latent
+    assert lazy.materialized and lat.shape == (4, 24, 1, 8)
+    z = lat[0].detach()
+    model.ode.clear_tracking()
+    with torch.no_grad():
+        ref = pkg.odeint(model.ode, z, t.to(DEV), method="rk4", options=dict(step_size=t[1] - t[0]))
+    assert torch.equal(lat.detach(), ref)
+    (lat[..., 1] * 0.5).sum().backward()                  # a loss built on the materialised latent
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in model.ode.parameters())
 
 
 @pytest.mark.gpu

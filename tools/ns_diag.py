@@ -22,6 +22,11 @@ def main():
     N = int(os.environ.get("DIAG_N", "512"))
     kind = os.environ.get("DIAG_KIND", "FaFp")
     horizons = [int(x) for x in os.environ.get("DIAG_T", "31,91,181,366").split(",")]
+    print(f"N={N} kind={kind} stats={os.environ.get('DIAG_STATS', '0')}", flush=True)
+    stats = os.environ.get("DIAG_STATS", "0") == "1"
+    DM = torch.tensor([0.3, -0.2], dtype=torch.float64)
+    DS = torch.tensor([0.5, 0.1], dtype=torch.float64)
+    DN = 0.1
     torch.manual_seed(0)
     kw = dict(net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]) if kind == "FaFp" else dict(net_sizes=[32, 32])
     mod = getattr(pkg, kind)(1, latent_dim=8, **kw)
@@ -43,13 +48,19 @@ def main():
                 lat = pkg.odeint(mg, yg, t, method="rk4", options=dict(step_size=t[1] - t[0]))
             else:
                 lat = eager_fixed_grid(mg, yg, t.cuda(), "rk4", t[1] - t[0])
-            (lat.double() * dl.cuda()).sum().backward()
+            loss = (lat.double() * dl.cuda()).sum()
+            if stats:
+                if mg.ode_type != "Fp":
+                    loss = loss + DN * torch.norm(torch.stack(mg.tracker))
+                post = mg.posterior()
+                loss = loss + (post.loc.double() * DM.cuda()).sum() + (post.scale.double() * DS.cuda()).sum()
+            loss.backward()
             res[name] = {"latent": lat.detach().cpu(), "y0": yg.grad.cpu(),
                          "w0": mg.ude_linears()[0].weight.grad.cpu(), "wl": mg.ude_linears()[-1].weight.grad.cpu()}
             mod.cpu()
         for dt, nm in ((torch.float64, "o64"), (torch.float32, "o32")):
             r = solve_and_grad_chunked(OracleRHS.from_module(mod, dt), y0.to(dt), t, t[1] - t[0], dl.to(dt),
-                                       chunk=64, workers=12)
+                                       *((DM.to(dt), DS.to(dt), DN) if stats else ()), chunk=64, workers=12)
             keys = [k for k in r.grads if k != "y0"]
             res[nm] = {"latent": r.latent, "y0": r.grads["y0"], "w0": r.grads[keys[0]], "wl": r.grads[keys[-2]]}
         ref = res["o64"]

@@ -43,7 +43,11 @@ def main():
             continue
         f_kib = sum(fe[k]) / len(fe[k])
         w_kib = sum(wr[k]) / len(wr[k])
+        import subprocess
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                                cwd=os.path.dirname(out_dir)).stdout.strip() or os.environ.get("UDE_COMMIT")
         rec = {"kernel": KERNELS[k], "workload": workload, "launches": [len(fe[k]), len(wr[k])],
+               "commit": commit,
                "FETCH_SIZE_KiB_avg": f_kib, "WRITE_SIZE_KiB_avg": w_kib,
                "hbm_bytes_per_launch": (f_kib + w_kib) * 1024.0,
                "hbm_bytes_per_launch_if_fetch_x2": (2.0 * f_kib + w_kib) * 1024.0,

@@ -196,6 +196,26 @@ def cpu_baseline(w, mod_gpu, budget_s=10.0, threads=1):
             "host_cpus_visible": os.cpu_count()}
 
 
+def cpu_baseline_child(workload, threads, timeout_s=150):
+    """cpu_baseline at `threads` threads in a child process with a time cap (oversubscribing the
+    host share can stall for minutes): the same sample and weights (seed 0) as the main baselines."""
+    import subprocess
+    code = ("import sys, json, torch; sys.path.insert(0, %r); import bench, importlib; "
+            "pkg = importlib.import_module(bench.PKG); w = bench.WORKLOADS[%r]; "
+            "m, _, _, _ = bench.build(pkg, w, torch.device('cpu'), seed=1000); "
+            "print(json.dumps(bench.cpu_baseline(w, m, budget_s=5.0, threads=%d)))" % (REPO, workload, threads))
+    print(f"[bench] cpu baseline at {threads} threads (child, cap {timeout_s} s)", file=sys.stderr, flush=True)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(threads))
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout_s, env=env)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except subprocess.TimeoutExpired:
+        return {"value": None, "cores": threads, "note": f"not finished within {timeout_s} s: {threads} threads "
+                "oversubscribe this box's CPU share (OMP_NUM_THREADS=%s)" % os.environ.get("OMP_NUM_THREADS")}
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "cores": threads, "note": f"failed: {e!r}"}
+
+
 def dopri5_line(pkg, w, dev, reps=3):
     """BASELINE configs[2] forward: the same batch solved by the fused adaptive dopri5
     (torchdiffeq defaults rtol 1e-7, atol 1e-9; evaluation path, no autograd)."""
@@ -580,11 +600,12 @@ def main():
             torch.cuda.empty_cache()
             print(f"[bench] {name}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.rehearse_cpu:
+        print("[bench] cpu baselines", file=sys.stderr, flush=True)
         res["cpu_baseline"] = cpu_baseline(w, mod, threads=CPU_THREADS)
         res["cpu_baseline_1thread"] = cpu_baseline(w, mod, threads=1)
         if (os.cpu_count() or 1) > CPU_THREADS:
             # also at every visible host core (more than this box's share per GPU)
-            res["cpu_baseline_all_visible_cores"] = cpu_baseline(w, mod, threads=os.cpu_count())
+            res["cpu_baseline_all_visible_cores"] = cpu_baseline_child(args.workload, os.cpu_count())
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

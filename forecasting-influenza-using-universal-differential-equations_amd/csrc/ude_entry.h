@@ -199,7 +199,7 @@ struct Ops {
       if (p->recompute) return Ops<Recompute<M>>::dec_backward(p, sched, ckpt, dyhat, W, grad_reg, ws, dl3, dW, db, s);
     }
     if (!sched || !ckpt || !dyhat || !W || !grad_reg || !ws || !dl3 || !dW || !db) return UDE_E_INVALID;
-    if (p->n_steps < 1) return UDE_E_INVALID;
+    if (p->n_steps < 1 || p->n_out + 1 > DecBwdDims<M>::MAX_T) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     const int n_tiles = (p->n_traj + TT - 1) / TT;

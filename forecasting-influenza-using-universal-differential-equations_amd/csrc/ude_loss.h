@@ -488,9 +488,16 @@ struct DecBwdDims {
   static constexpr int NFT = KP / 16, NRT = NP / 16;
   static constexpr int NDW = NFT * NRT;                // dW tiles (r tile, f tile)
   static constexpr int dw_of(int w) { return (NDW + WAVES - 1 - w) / WAVES; }
-  static constexpr int LDS = (KP * WS + TT * YS + TT * DS + TT * YS) * 4;
+  static constexpr int MAX_T = 2048;                   // output times (grid-point table in LDS)
+  static constexpr int LDS = (KP * WS + TT * YS + TT * DS + TT * YS) * 4 + MAX_T * 4;
+  // per-thread register prefetch of the next (tile, output) item
+  static constexpr int PY = (M::F * TT + NTHREADS - 1) / NTHREADS;
+  static constexpr int PD = (TT * M::R + NTHREADS - 1) / NTHREADS;
 };
 
+// Work items (tile, output) in tile-major order, persistent over the grid; the next item's y block
+// and d y_hat rows are loaded into registers while the current one computes (its HBM latency
+// hidden behind the item's two GEMMs).
 template <class M, int W>
 __device__ void dec_bwd_body(const DecBwdArgs& A, float* lds) {
   using Q = DecBwdDims<M>;
@@ -500,7 +507,9 @@ __device__ void dec_bwd_body(const DecBwdArgs& A, float* lds) {
   float* Yt = Wl + Q::KP * Q::WS;        // [16][YS]  output state y[t][f]
   float* Dy = Yt + TT * Q::YS;           // [16][DS]  d y_hat[t][r]
   float* Cs = Dy + TT * Q::DS;           // [16][YS]  d y[t][f] staging
+  int* kof = reinterpret_cast<int*>(Cs + TT * Q::YS);   // grid point of output jo
   const Sched sc(A.sched, A.n_steps, A.n_out);
+  const int T = A.n_out + 1;
   const float g_reg = *A.grad_reg;
   #pragma unroll 1
   for (int i = tid; i < Q::KP * Q::WS; i += NTHREADS) {
@@ -511,74 +520,92 @@ __device__ void dec_bwd_body(const DecBwdArgs& A, float* lds) {
   for (int i = tid; i < TT * Q::YS; i += NTHREADS) Yt[i] = 0.f;
   #pragma unroll 1
   for (int i = tid; i < TT * Q::DS; i += NTHREADS) Dy[i] = 0.f;
+  if (tid == 0) {
+    // output 0 is y0 (grid point 0); every other output is a grid hit after its step
+    kof[0] = 0;
+    for (int st = 0; st < A.n_steps; ++st)
+      for (int o = sc.out_start[st]; o < sc.out_start[st + 1]; ++o) kof[sc.out_j[o]] = st + 1;
+  }
   f4 dw[Q::dw_of(W) > 0 ? Q::dw_of(W) : 1];
 #pragma unroll
   for (int i = 0; i < Q::dw_of(W); ++i) dw[i] = f4zero();
   float db = 0.f;                        // thread r < NP: d b_dec partial
   const size_t fin = ckpt_final_off<M>(A.n_tiles, A.n_steps);
+  __syncthreads();
 
-  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
-    const int n0 = tile * TT;
-    const int nv = min(TT, A.n_traj - n0);
-    // outputs in order: output 0 at grid point 0, then each step's (mode 1) output at step + 1
-    int step = -1, o = 0;
-    #pragma unroll 1
-    while (true) {
-      int jo, k;
-      if (step < 0) {
-        jo = 0; k = 0; step = 0; o = sc.out_start[0];
-      } else {
-        while (step < A.n_steps && o >= sc.out_start[step + 1]) ++step;
-        if (step >= A.n_steps) break;
-        jo = sc.out_j[o]; k = step + 1; ++o;
-      }
-      __syncthreads();                   // previous output's Cs copied, Yt / Dy reads done
-      // y block [F][16] of grid point k -> Yt[t][f]; d y_hat rows -> Dy[t][r]
-      const float* yb = k < A.n_steps ? A.ckpt + ckpt_index(tile, A.n_steps, k, 0, F, 0, 0)
-                                      : A.ckpt + fin + (size_t)tile * F * TT;
-      #pragma unroll 4
-      for (int i = tid; i < F * TT; i += NTHREADS) {
-        const int f = i >> 4, t = i & 15;
-        Yt[t * Q::YS + f] = yb[i];
-      }
-      const float* dyr = A.dyhat + ((size_t)jo * A.n_traj + n0) * R;
-      #pragma unroll 4
-      for (int i = tid; i < TT * R; i += NTHREADS) {
+  float py[Q::PY], pd[Q::PD];
+  const long n_items = (long)A.n_tiles * T;
+  auto fetch = [&](long item) {
+    const int tile = (int)(item / T), jo = (int)(item - (long)tile * T);
+    const int k = kof[jo];
+    const float* yb = k < A.n_steps ? A.ckpt + ckpt_index(tile, A.n_steps, k, 0, F, 0, 0)
+                                    : A.ckpt + fin + (size_t)tile * F * TT;
+#pragma unroll
+    for (int u = 0; u < Q::PY; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < F * TT) py[u] = yb[i];
+    }
+    const int n0 = tile * TT, nv = min(TT, A.n_traj - n0);
+    const float* dyr = A.dyhat + ((size_t)jo * A.n_traj + n0) * R;
+#pragma unroll
+    for (int u = 0; u < Q::PD; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < TT * R) pd[u] = i < nv * R ? dyr[i] : 0.f;
+    }
+  };
+  if ((long)blockIdx.x < n_items) fetch(blockIdx.x);
+  for (long item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const int tile = (int)(item / T), jo = (int)(item - (long)tile * T);
+    const int n0 = tile * TT, nv = min(TT, A.n_traj - n0);
+    __syncthreads();                     // previous item's Cs copied, Yt / Dy reads done
+#pragma unroll
+    for (int u = 0; u < Q::PY; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < F * TT) Yt[(i & 15) * Q::YS + (i >> 4)] = py[u];
+    }
+#pragma unroll
+    for (int u = 0; u < Q::PD; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < TT * R) {
         const int t = i / R, r = i - t * R;
-        Dy[t * Q::DS + r] = t < nv ? dyr[i] : 0.f;
+        Dy[t * Q::DS + r] = pd[u];
       }
-      __syncthreads();
-      // d W_dec tiles (rows r, cols f; K = the tile's 16 trajectories) and d b_dec
+    }
+    __syncthreads();
+    if (item + (long)gridDim.x < n_items) fetch(item + gridDim.x);
+    // d W_dec tiles (rows r, cols f; K = the tile's 16 trajectories) and d b_dec
 #pragma unroll
-      for (int i = 0; i < Q::dw_of(W); ++i) {
-        const int id = W + WAVES * i, rt = id / Q::NFT, ft = id - rt * Q::NFT;
+    for (int i = 0; i < Q::dw_of(W); ++i) {
+      const int id = W + WAVES * i, rt = id / Q::NFT, ft = id - rt * Q::NFT;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          dw[i] = mfma4(Dy[(4 * q + g) * Q::DS + rt * 16 + t16], Yt[(4 * q + g) * Q::YS + ft * 16 + t16], dw[i]);
+      for (int q = 0; q < 4; ++q)
+        dw[i] = mfma4(Dy[(4 * q + g) * Q::DS + rt * 16 + t16], Yt[(4 * q + g) * Q::YS + ft * 16 + t16], dw[i]);
+    }
+    if (tid < Q::NP) {
+#pragma unroll
+      for (int t = 0; t < TT; ++t) db += Dy[t * Q::DS + tid];
+    }
+    // d y^T tiles (rows f, cols t; K = the R decoder outputs) + latent_init_loss'
+    for (int ft = W; ft < Q::NFT; ft += WAVES) {
+      f4 acc = f4zero(), acc2 = f4zero();
+#pragma unroll
+      for (int q = 0; q < Q::NP / 4; q += 2) {
+        acc = mfma4(Wl[(ft * 16 + t16) * Q::WS + 4 * q + g], Dy[t16 * Q::DS + 4 * q + g], acc);
+        acc2 = mfma4(Wl[(ft * 16 + t16) * Q::WS + 4 * q + 4 + g], Dy[t16 * Q::DS + 4 * q + 4 + g], acc2);
       }
-      if (tid < Q::NP) {
+      acc += acc2;
+      const f4 y = *reinterpret_cast<const f4*>(Yt + t16 * Q::YS + ft * 16 + 4 * g);
 #pragma unroll
-        for (int t = 0; t < TT; ++t) db += Dy[t * Q::DS + tid];
-      }
-      // d y^T tiles (rows f, cols t; K = the R decoder outputs) + latent_init_loss'
-      for (int ft = W; ft < Q::NFT; ft += WAVES) {
-        f4 acc = f4zero();
-#pragma unroll
-        for (int q = 0; q < Q::NP / 4; ++q)
-          acc = mfma4(Wl[(ft * 16 + t16) * Q::WS + 4 * q + g], Dy[t16 * Q::DS + 4 * q + g], acc);
-        const f4 y = *reinterpret_cast<const f4*>(Yt + t16 * Q::YS + ft * 16 + 4 * g);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] += g_reg * (y[e] < 0.f ? -1.f : (y[e] > 1.f ? 1.f : 0.f));
-        *reinterpret_cast<f4*>(Cs + t16 * Q::YS + ft * 16 + 4 * g) = acc;
-      }
-      __syncthreads();
-      // the tile's (16, 3R) block of d latent[..., :3] at output jo is contiguous
-      float* dst = A.dl3 + ((size_t)jo * A.n_traj + n0) * F;
-      #pragma unroll 4
-      for (int i = tid; i < nv * F; i += NTHREADS) {
-        const int t = i / F, f = i - t * F;
-        dst[i] = Cs[t * Q::YS + f];
-      }
+      for (int e = 0; e < 4; ++e) acc[e] += g_reg * (y[e] < 0.f ? -1.f : (y[e] > 1.f ? 1.f : 0.f));
+      *reinterpret_cast<f4*>(Cs + t16 * Q::YS + ft * 16 + 4 * g) = acc;
+    }
+    __syncthreads();
+    // the tile's (16, 3R) block of d latent[..., :3] at output jo is contiguous
+    float* dst = A.dl3 + ((size_t)jo * A.n_traj + n0) * F;
+    #pragma unroll 4
+    for (int i = tid; i < nv * F; i += NTHREADS) {
+      const int t = i / F, f = i - t * F;
+      dst[i] = Cs[t * Q::YS + f];
     }
   }
   float* my = A.slab + (size_t)blockIdx.x * LossDims<R>::SLAB;
@@ -617,12 +644,31 @@ __global__ __launch_bounds__(256) void ude_nll_fwd_kernel(const float* __restric
     const int r = gid % R, tb = gid / R, b = tb % B, t = tb / B;
     const size_t stride = (size_t)B * R;
     const float* p = yhat + (size_t)t * S * stride + (size_t)b * R + r;
+    // samples in batches of 8 independent loads (the strided reads are latency-bound one by one)
     double s1 = 0.0;
-    for (int s = 0; s < S; ++s) s1 += (double)p[s * stride];
+    int s = 0;
+    for (; s + 8 <= S; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(s + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s1 += (double)v[u];
+    }
+    for (; s < S; ++s) s1 += (double)p[(size_t)s * stride];
     const float mu = (float)(s1 / (double)S);
     double s2 = 0.0;
-    for (int s = 0; s < S; ++s) {
-      const float d = p[s * stride] - mu;
+    for (s = 0; s + 8 <= S; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(s + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float d = v[u] - mu;
+        s2 += (double)(d * d);
+      }
+    }
+    for (; s < S; ++s) {
+      const float d = p[(size_t)s * stride] - mu;
       s2 += (double)(d * d);
     }
     const float sd = sqrtf((float)(s2 / (double)(S - 1)));

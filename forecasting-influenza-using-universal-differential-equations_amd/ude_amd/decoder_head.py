@@ -24,6 +24,9 @@ from . import _native
 from . import fused as _fused
 
 
+MAX_TIMES = 2048          # output times the decoder backward's grid-point table holds (DecBwdDims::MAX_T)
+
+
 def decoder_linear(dec) -> Optional[torch.nn.Linear]:
     """The Linear(3R -> R) of a reference Decoder (lib/models.py:37-40), else None."""
     seq = getattr(dec, "decoder", None)
@@ -68,7 +71,7 @@ def solve_decode(ode, y0: torch.Tensor, t: torch.Tensor, step_size, linear: torc
     time that is not a grid point (the epilogue needs exact hits: torchdiffeq mode y(t1))."""
     from . import solvers
     plan = solvers.plan_for(ode, y0, t, step_size)
-    if plan.out_k is None:
+    if plan.out_k is None or plan.n_times > MAX_TIMES:
         return None
     params = []
     for lin in ode.ude_linears():

@@ -240,7 +240,8 @@ int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, c
  * of ude_rk4_forward but emits, at every output time, y_hat (T, N, R) = W_dec . y[:3R] + b_dec
  * (y_pred = y_hat.reshape(T, S, B, R).permute(2, 1, 0, 3)) and reg_out (device float) =
  * latent_init_loss over every output's S, I, R, and writes no (T, N, R, L) latent.  Every output
- * time must be a grid point (torchdiffeq exact hit: schedule mode 1) and n_steps >= 1.
+ * time must be a grid point (torchdiffeq exact hit: schedule mode 1), n_steps >= 1 and
+ * T <= 2048 (ude_decoder_backward returns UDE_E_INVALID otherwise).
  *   dec_pack: ude_query's dec_pack_bytes, filled by ude_pack_decoder(W_dec (R, 3R), b_dec (R));
  *   ckpt: ckpt_bytes + ckpt_final_bytes (the final state is stored behind the checkpoints);
  *   stats_slab: stats_slab_bytes; reg_slab: grid_fwd doubles.

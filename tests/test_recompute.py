@@ -66,8 +66,15 @@ def test_recompute_bit_identical_and_vs_oracle(pkg, case):
     assert a[0] == 0 and a[1] > 0, "default plan stores activations"
     assert b[0] == 1 and b[1] == 0, "a zero budget selects the recompute path"
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]), "latent / dy0 differ"
+    # weight gradients: bit-identical where both backwards accumulate them the same way (R = 49);
+    # small records' stored path is the 8-wave split kernel, whose partner waves sum the bias rows
+    # per trajectory first (a different fp32 summation order than the 4-wave recompute kernel)
+    split = R <= 16
     for ga, gb in zip(a[4], b[4]):
-        assert torch.equal(ga, gb)
+        if split:
+            assert normwise_rel(gb, ga) < 1e-6
+        else:
+            assert torch.equal(ga, gb)
     ref = solve_and_grad(OracleRHS.from_module(mod.cpu(), torch.float64), y0.double(), t, t[1] - t[0],
                          dl.double(), torch.tensor([0.3, -0.2], dtype=torch.float64),
                          torch.tensor([0.5, 0.1], dtype=torch.float64), 0.1 if kind != "Fp" else None)

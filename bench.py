@@ -493,6 +493,7 @@ def main():
                     help="weak: every rank solves the workload's batch; strong: the batch is split over ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--lines", default=None, help="comma-separated subset of the extra lines (development)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for runs; gloo only to rehearse N>1")
     ap.add_argument("--rehearse-cpu", action="store_true",
                     help="plumbing rehearsal on the host (gloo, eager solver): checks ranks / batch accounting")
@@ -594,6 +595,9 @@ def main():
                  ("bayes_state49", lambda: bayes_large_line(pkg, dev)),
                  ("loss_head_state49", lambda: loss_head_line(pkg, w, dev)),
                  ("train_step_head_state49", lambda: train_head_line(pkg, w, dev))]
+        if args.lines:
+            keep = set(args.lines.split(","))
+            lines = [(n, f) for n, f in lines if n in keep]
         for name, fn in lines:
             t0 = time.perf_counter()
             res[name] = fn()

@@ -1436,10 +1436,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
   }
 
-  // SPLIT_BWD: the weight-gradient accumulators live on the partner waves (bwd_wbody)
-  f4 dw[M::SPLIT_BWD ? 1 : NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
+  // SPLITB: the weight-gradient accumulators live on the partner waves (bwd_wbody / bwd_wbody_l)
+  f4 dw[M::SPLITB ? 1 : NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
 #pragma unroll
-  for (int i = 0; i < (M::SPLIT_BWD ? 1 : NDWn); ++i) dw[i] = f4zero();
+  for (int i = 0; i < (M::SPLITB ? 1 : NDWn); ++i) dw[i] = f4zero();
   if constexpr (M::BAYES) {
 #pragma unroll
     for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
@@ -1462,7 +1462,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
-    load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    // the record's static features feed only the static hoist of a recomputed forward (and FULL0's
+    // layer 0); with stored activations their alias of the activation region must stay untouched
+    // (the SPLIT_BWD_L partner waves fill it by LDS-DMA meanwhile)
+    if constexpr (!M::ACT_STORED || M::FULL0) load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
     if constexpr (M::FULL0) {
       #pragma unroll 1
       for (int i = tid; i < TT * M::S16; i += NTHREADS) {
@@ -1549,7 +1552,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if constexpr (M::STORE_ACT_D) {
           if (jj == 0 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvs);
         }
-        if constexpr (M::STORE_ACT_D && UDE_ABL != 8) {
+        if constexpr (M::STORE_ACT_D && !M::SPLIT_BWD_L && UDE_ABL != 8) {
           // this stage's activation rows straight from the forward's store (issued first: the
           // stage-input copy below runs under their latency)
           constexpr int QR = M::ACT_A4 / 4;
@@ -1571,6 +1574,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         }
         if constexpr (M::SPLIT_BWD) {
           // stage input, activation rows and output cotangents: the partner waves' (bwd_wbody)
+        } else if constexpr (M::SPLIT_BWD_L) {
+          // stage input and activation rows: the partner waves' (bwd_wbody_l)
         } else if (CARRY && have_next && UDE_ABL != 4) {
           constexpr int QR = M::ACT_A4 / 4;
 #pragma unroll
@@ -1713,7 +1718,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
-        if (!EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        if (!M::SPLIT_BWD_L && !EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (!M::SPLIT_BWD && next_out) {
@@ -1735,7 +1740,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 17);
-        if (!CARRY && have_next) {
+        if (!CARRY && !M::SPLIT_BWD_L && have_next) {
           sfor<SL>([&](auto ss) {
             constexpr int sl = decltype(ss)::value;
             const int p = tid + sl * NTHREADS;
@@ -1751,7 +1756,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         lds_sync();
         UDE_STAMP(pf, 11);
         if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { lds_sync(); });
-        else mlp_backward<M, W, SR, M::SPLIT_BWD>(rse, es, lds, dw, dws, g0t, lane, pf,
+        else mlp_backward<M, W, SR, M::SPLITB>(rse, es, lds, dw, dws, g0t, lane, pf,
                                              RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
         if constexpr (M::SPLITX0) {
           // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
@@ -1834,14 +1839,14 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     // per-trajectory layer-0 gradient sums -> global (static-feature gradients are
     // computed from them by ude_static_*_kernel); their trajectory sums -> bias row sums
     // (BAYES: layer-0 bias and static columns were accumulated per evaluation instead)
-    if constexpr (!M::BAYES && !M::SPLIT_BWD) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
+    if constexpr (!M::BAYES && !M::SPLITB) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
     lds_sync();
   }
 
   // ---- kernel end: register tiles + LDS row sums -> this workgroup's slab ----
-  if constexpr (!M::SPLIT_BWD) dw_to_slab<M, W>(dw, dws, myslab, lane);
-  // SPLIT_BWD: the partner waves' last bias row sums land before this barrier
-  if constexpr (M::SPLIT_BWD) lds_sync();
+  if constexpr (!M::SPLITB) dw_to_slab<M, W>(dw, dws, myslab, lane);
+  // SPLITB: the partner waves' last bias row sums land before this barrier
+  if constexpr (M::SPLITB) lds_sync();
   #pragma unroll 1
   for (int i = tid; i < M::NDB; i += NTHREADS) {
     myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
@@ -1969,6 +1974,188 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
   lds_sync();                            // bias row sums complete -> bwd_body copies them
 }
 
+
+// ---- SPLIT_BWD_L: the partner waves of large records ------------------------------------
+// Barrier for waves with LDS-DMA loads in flight: their LDS writes are retired by lgkmcnt, the
+// DMA (which counts on vmcnt) stays in flight across it (lds_sync's release fence would drain it,
+// holding the critical-path waves at this barrier for the HBM latency).
+__device__ __forceinline__ void lds_sync_dma() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);          // lgkmcnt(0) only
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void wait_dma() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
+}
+typedef __attribute__((address_space(3))) void* LdsPtr;
+
+// LDS-DMA of one layer's activation rows (net, i) of tile-stage (step, jj) into the record:
+// partner wave W moves trajectories 4W .. 4W+3, one 16-B-per-lane instruction each (kout / 4
+// lanes; the record row's layer slice is contiguous, so the lane-linear destination fits).
+template <class M, int W, int net, int i>
+__device__ __forceinline__ void dma_layer(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
+  constexpr int SR = M::SR_B, KO = M::kout(net, i), OFF = M::act_off(net, i);
+  const float* src = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = 4 * W + u;
+    if (lane < KO / 4)
+      __builtin_amdgcn_global_load_lds((const void*)(src + t * M::ACT_A4 + (OFF - M::ACT0) + 4 * lane),
+                                       (LdsPtr)(lds + t * SR + OFF), 16, 0, 0);
+  }
+}
+// the layers whose last reader of the current stage is phase d (d = D: the flux pass)
+template <class M, int W, int d>
+__device__ __forceinline__ void dma_freed(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
+  sfor<2>([&](auto nn) {
+    constexpr int net = decltype(nn)::value;
+    if constexpr (d == M::D) {
+      if constexpr (M::has(net, 0)) dma_layer<M, W, net, M::nl(net) - 1>(A, lds, tile, step, jj, lane);
+    } else if constexpr (d >= 1 && M::has(net, d) && d - 1 < M::nl(net) - 1) {
+      dma_layer<M, W, net, d - 1>(A, lds, tile, step, jj, lane);
+    }
+  });
+}
+// LDS-DMA of the checkpointed stage input ([F][16], contiguous) into the staging slot
+template <class M, int W>
+__device__ __forceinline__ void dma_ckpt(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
+  constexpr int NF = M::F * TT, NC = (NF + 255) / 256;
+  const float* src = A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0);
+#pragma unroll
+  for (int c = W; c < NC; c += WAVES)
+    if (c * 256 + 4 * lane < NF)
+      __builtin_amdgcn_global_load_lds((const void*)(src + c * 256 + 4 * lane), (LdsPtr)(lds + M::STG_LDS + c * 256),
+                                       16, 0, 0);
+}
+
+// Weight gradients of one stage (large records): as mlp_backward_dw, with each owned tile's input
+// operands read in chunks of XC column tiles (registers: the dW accumulators fill this wave) and the
+// bias sums reduced across the tile's trajectories into the LDS row sums every phase.
+template <class M, int W, int SR, class After>
+__device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, int lane, const After& after) {
+  const int t = lane & 15, g = lane >> 4;
+  const float* rec = lds + t * SR;
+  constexpr int XC = 4;
+  sfor<M::D>([&](auto ee) {
+    constexpr int d = M::D - 1 - decltype(ee)::value;
+    sfor<M::FT(d)>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if constexpr (M::fowner(d, k) == W) {
+        constexpr int net = M::fnet(d, k), rt = M::frt(d, k), goff = M::gbuf(net, d);
+        constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
+        constexpr int NC = M::rti(net, d);
+        const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
+        float ga[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
+        sfor<(NC + XC - 1) / XC>([&](auto cc0) {
+          constexpr int c0 = decltype(cc0)::value * XC;
+          constexpr int NCC = cmin(XC, NC - c0);
+          float bv[4][NCC];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int ct = 0; ct < NCC; ++ct) bv[s][ct] = lds[(4 * g + s) * SR + inoff + (c0 + ct) * 16 + t];
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            sfor<NCC>([&](auto cc) {
+              constexpr int ct = decltype(cc)::value;
+              constexpr int idx = M::ndw_before(W, d, k) + c0 + ct;
+              dw[idx] = mfma4(ga[s], bv[s][ct], dw[idx]);
+            });
+        });
+        if constexpr (d == 0) {
+          g0t[M::nz_before(W, k)] += gv;
+        } else {
+          f4 r = gv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
+            r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
+          }
+          if (t == 0) {
+            float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
+            db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
+          }
+        }
+      }
+    });
+    lds_sync_dma();
+    after(std::integral_constant<int, d>{});
+  });
+}
+
+// SPLIT_BWD_L partner wave W + 4: weight gradients of every stage and the next stage's data
+// (LDS-DMA), on the exact barrier sequence of bwd_body's critical-path waves.
+template <class M, int W>
+__device__ void bwd_wbody_l(const KArgs& A, float* lds) {
+  constexpr int SR = M::SR_B;
+  constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
+  constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  const int lane = threadIdx.x & 63;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
+  f4 dw[NDWn], g0t[NZn];
+#pragma unroll
+  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  lds_sync();                                           // record zeroed
+  // staged stage input [f][t] -> Y slot [t][f]: each wave moves exactly the 256-float chunks its own
+  // dma_ckpt wrote (its vmcnt wait covers only its own DMAs; the other waves' may still be landing)
+  auto put_stage = [&]() {
+    constexpr int NF = M::F * TT, NC = (NF + 255) / 256;
+#pragma unroll
+    for (int c = W; c < NC; c += WAVES)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = c * 256 + e * 64 + lane;
+        if (i < NF) lds[(i & 15) * SR + M::Y_OFF + (i >> 4)] = lds[M::STG_LDS + i];
+      }
+  };
+  auto dma_all = [&](int tile_, int step_, int jj_) {
+    sfor<2>([&](auto nn) {
+      constexpr int net = decltype(nn)::value;
+      sfor<M::nl(net)>([&](auto ii) { dma_layer<M, W, net, decltype(ii)::value>(A, lds, tile_, step_, jj_, lane); });
+    });
+    dma_ckpt<M, W>(A, lds, tile_, step_, jj_, lane);
+  };
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    // the tile's first stage: everything at once (nothing of it is in the record yet)
+    if (A.n_steps > 0) dma_all(tile, A.n_steps - 1, 3);
+    lds_sync_dma();                                     // last step's output cotangents staged
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    lds_sync_dma();
+    for (int step = A.n_steps - 1; step >= 0; --step) {
+      #pragma unroll 1
+      for (int jj = 3; jj >= 0; --jj) {
+        const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
+        const bool have = nstep >= 0;
+        wait_dma();                                     // this stage's rows and input have landed
+        put_stage();
+        lds_sync_dma();                                 // stage input + activation rows in the record
+        if (have) dma_ckpt<M, W>(A, lds, tile, nstep, njj, lane);   // staging slot free again
+        lds_sync_dma();                                 // flux pass: final-layer gradients written
+        if (have) dma_freed<M, W, M::D>(A, lds, tile, nstep, njj, lane);
+        mlp_backward_dw_l<M, W, SR>(lds, dw, g0t, lane, [&](auto dd) {
+          constexpr int d = decltype(dd)::value;
+          if constexpr (d >= 1)
+            if (have) dma_freed<M, W, d>(A, lds, tile, nstep, njj, lane);
+        });
+      }
+    }
+    lds_sync_dma();                                     // tile end: dy0
+    lds_sync_dma();
+    g0_tile_end<M, W>(A, lds, g0t, tile, lane);
+    lds_sync_dma();
+  }
+  wait_dma();
+  f4 none[1];
+  dw_to_slab<M, W>(dw, none, myslab, lane);
+  lds_sync();                                           // bias row sums complete -> bwd_body copies them
+}
+
 template <class M>
 __global__ __launch_bounds__(M::BWD_THREADS) void ude_bwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1979,6 +2166,15 @@ __global__ __launch_bounds__(M::BWD_THREADS) void ude_bwd_kernel(KArgs a) {
       else if (w == 5) bwd_wbody<M, 1>(a, lds);
       else if (w == 6) bwd_wbody<M, 2>(a, lds);
       else bwd_wbody<M, 3>(a, lds);
+      return;
+    }
+  }
+  if constexpr (M::SPLIT_BWD_L) {
+    if (w >= WAVES) {
+      if (w == 4) bwd_wbody_l<M, 0>(a, lds);
+      else if (w == 5) bwd_wbody_l<M, 1>(a, lds);
+      else if (w == 6) bwd_wbody_l<M, 2>(a, lds);
+      else bwd_wbody_l<M, 3>(a, lds);
       return;
     }
   }

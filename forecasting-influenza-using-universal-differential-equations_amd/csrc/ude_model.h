@@ -173,7 +173,18 @@ struct Model {
   // in the stage waits for) from the same LDS operands, on the same SIMDs, so their MFMAs fill
   // the critical path's gaps.
   static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !BAYES;
-  static constexpr int BWD_THREADS = SPLIT_BWD ? 2 * NTHREADS : NTHREADS;
+  // Large records (STORE_ACT_D) split the same way (SPLIT_BWD_L): waves 4-7 (bwd_wbody_l) hold the
+  // weight-gradient accumulators (the ~176 VGPRs per wave that kept the 4-wave kernel at one wave per
+  // SIMD) and move the next stage's data with LDS-DMA (global_load_lds): each layer's activation rows
+  // as soon as the current stage's last reader of that layer is past its barrier, and the checkpointed
+  // stage input into the staging slot -- no data registers, no exposed load at the stage start.
+#ifndef UDE_NO_SPLIT_L
+  static constexpr bool SPLIT_BWD_L = STORE_ACT_D && !BAYES;
+#else
+  static constexpr bool SPLIT_BWD_L = false;
+#endif
+  static constexpr bool SPLITB = SPLIT_BWD || SPLIT_BWD_L;
+  static constexpr int BWD_THREADS = SPLITB ? 2 * NTHREADS : NTHREADS;
   // Training forward of small records at one tile per CU: four more waves copy each stage's
   // activation rows from the record to HBM during the flux pass, off the critical path
   // (ude_kernels.h fwd_sbody).  With more tiles than CUs two 4-wave workgroups per CU win.
@@ -376,7 +387,7 @@ struct Model {
 template <class B>
 struct Recompute : B {
   static constexpr bool STORE_ACT = false, STORE_ACT_D = false, ACT_STORED = false;
-  static constexpr bool SPLIT_BWD = false, SPLIT_FWD = false;
+  static constexpr bool SPLIT_BWD = false, SPLIT_FWD = false, SPLIT_BWD_L = false, SPLITB = false;
   static constexpr int BWD_THREADS = NTHREADS;
   static constexpr int LDS_B = B::ACT_STG * 4;
   static constexpr int LDS_F_DEC = B::LDS_F + NTHREADS * 8;

@@ -1994,28 +1994,38 @@ typedef __attribute__((address_space(3))) void* LdsPtr;
 
 // LDS-DMA of one layer's activation rows (net, i) of tile-stage (step, jj) into the record:
 // partner wave W moves trajectories 4W .. 4W+3, one 16-B-per-lane instruction each (kout / 4
-// lanes; the record row's layer slice is contiguous, so the lane-linear destination fits).
+// lanes; the record row's layer slice is contiguous, so the lane-linear destination fits).  The
+// source goes through a buffer resource: SGPR base of the tile-stage block, one shared per-lane
+// offset (16 lane) and the slice's constant offset in the scalar soffset.  Per-instruction
+// per-lane addresses held in VGPRs spilled, and every spill reload (a vmcnt wait) drained all
+// DMAs in flight.
 template <class M, int W, int net, int i>
-__device__ __forceinline__ void dma_layer(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
+__device__ __forceinline__ void dma_layer(Rsrc src, float* lds, int lane) {
+  if constexpr (UDE_ABL == 22) return;
   constexpr int SR = M::SR_B, KO = M::kout(net, i), OFF = M::act_off(net, i);
-  const float* src = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int t = 4 * W + u;
+#if defined(__HIP_DEVICE_COMPILE__)
     if (lane < KO / 4)
-      __builtin_amdgcn_global_load_lds((const void*)(src + t * M::ACT_A4 + (OFF - M::ACT0) + 4 * lane),
-                                       (LdsPtr)(lds + t * SR + OFF), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (LdsPtr)(lds + t * SR + OFF), 16, 16 * lane,
+                                               (t * M::ACT_A4 + (OFF - M::ACT0)) * 4, 0, 0);
+#endif
   }
+}
+template <class M>
+__device__ __forceinline__ Rsrc act_rsrc(const KArgs& A, int tile, int step, int jj) {
+  return make_rsrc(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj), TT * M::ACT_A4 * 4);
 }
 // the layers whose last reader of the current stage is phase d (d = D: the flux pass)
 template <class M, int W, int d>
-__device__ __forceinline__ void dma_freed(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
+__device__ __forceinline__ void dma_freed(Rsrc src, float* lds, int lane) {
   sfor<2>([&](auto nn) {
     constexpr int net = decltype(nn)::value;
     if constexpr (d == M::D) {
-      if constexpr (M::has(net, 0)) dma_layer<M, W, net, M::nl(net) - 1>(A, lds, tile, step, jj, lane);
+      if constexpr (M::has(net, 0)) dma_layer<M, W, net, M::nl(net) - 1>(src, lds, lane);
     } else if constexpr (d >= 1 && M::has(net, d) && d - 1 < M::nl(net) - 1) {
-      dma_layer<M, W, net, d - 1>(A, lds, tile, step, jj, lane);
+      dma_layer<M, W, net, d - 1>(src, lds, lane);
     }
   });
 }
@@ -2023,12 +2033,15 @@ __device__ __forceinline__ void dma_freed(const KArgs& A, float* lds, int tile, 
 template <class M, int W>
 __device__ __forceinline__ void dma_ckpt(const KArgs& A, float* lds, int tile, int step, int jj, int lane) {
   constexpr int NF = M::F * TT, NC = (NF + 255) / 256;
-  const float* src = A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0);
+  const Rsrc src = make_rsrc(A.ckpt + ckpt_index(tile, A.n_steps, step, jj, M::F, 0, 0), NF * 4);
 #pragma unroll
-  for (int c = W; c < NC; c += WAVES)
+  for (int c = W; c < NC; c += WAVES) {
+#if defined(__HIP_DEVICE_COMPILE__)
     if (c * 256 + 4 * lane < NF)
-      __builtin_amdgcn_global_load_lds((const void*)(src + c * 256 + 4 * lane), (LdsPtr)(lds + M::STG_LDS + c * 256),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (LdsPtr)(lds + M::STG_LDS + c * 256), 16, 16 * lane, c * 1024,
+                                               0, 0);
+#endif
+  }
 }
 
 // Weight gradients of one stage (large records): as mlp_backward_dw, with each owned tile's input
@@ -2051,7 +2064,7 @@ __device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, i
         float ga[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
-        sfor<(NC + XC - 1) / XC>([&](auto cc0) {
+        if constexpr (UDE_ABL != 21) sfor<(NC + XC - 1) / XC>([&](auto cc0) {
           constexpr int c0 = decltype(cc0)::value * XC;
           constexpr int NCC = cmin(XC, NC - c0);
           float bv[4][NCC];
@@ -2114,9 +2127,10 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
       }
   };
   auto dma_all = [&](int tile_, int step_, int jj_) {
+    const Rsrc src = act_rsrc<M>(A, tile_, step_, jj_);
     sfor<2>([&](auto nn) {
       constexpr int net = decltype(nn)::value;
-      sfor<M::nl(net)>([&](auto ii) { dma_layer<M, W, net, decltype(ii)::value>(A, lds, tile_, step_, jj_, lane); });
+      sfor<M::nl(net)>([&](auto ii) { dma_layer<M, W, net, decltype(ii)::value>(src, lds, lane); });
     });
     dma_ckpt<M, W>(A, lds, tile_, step_, jj_, lane);
   };
@@ -2137,11 +2151,11 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
         lds_sync_dma();                                 // stage input + activation rows in the record
         if (have) dma_ckpt<M, W>(A, lds, tile, nstep, njj, lane);   // staging slot free again
         lds_sync_dma();                                 // flux pass: final-layer gradients written
-        if (have) dma_freed<M, W, M::D>(A, lds, tile, nstep, njj, lane);
+        if (have) dma_freed<M, W, M::D>(act_rsrc<M>(A, tile, nstep, njj), lds, lane);
         mlp_backward_dw_l<M, W, SR>(lds, dw, g0t, lane, [&](auto dd) {
           constexpr int d = decltype(dd)::value;
           if constexpr (d >= 1)
-            if (have) dma_freed<M, W, d>(A, lds, tile, nstep, njj, lane);
+            if (have) dma_freed<M, W, d>(act_rsrc<M>(A, tile, nstep, njj), lds, lane);
         });
       }
     }

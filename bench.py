@@ -196,7 +196,7 @@ def cpu_baseline(w, mod_gpu, budget_s=10.0, threads=1):
             "host_cpus_visible": os.cpu_count()}
 
 
-def cpu_baseline_child(workload, threads, timeout_s=150):
+def cpu_baseline_child(workload, threads, timeout_s=45):
     """cpu_baseline at `threads` threads in a child process with a time cap (oversubscribing the
     host share can stall for minutes): the same sample and weights (seed 0) as the main baselines."""
     import subprocess

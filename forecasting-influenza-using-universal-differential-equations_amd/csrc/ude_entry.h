@@ -8,6 +8,7 @@
 #include "ude_dopri5.h"
 #include "ude_loss.h"
 #include "ude_eval.h"
+#include "ude_gst.h"
 
 namespace ude {
 
@@ -59,6 +60,9 @@ struct Ops {
     if (M::HOIST)
       HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  DY0_STATIC_LDS));
+    if constexpr (M::GST)
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_gst_dw_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 Gst<M>::LDS));
     done = true;
     return UDE_OK;
   }
@@ -90,8 +94,17 @@ struct Ops {
   // BAYES: one weight sample per RHS evaluation (4 per RK4 step)
   static int64_t n_evals(const UdeProblem* p) { return M::BAYES ? 4 * (int64_t)p->n_steps : 1; }
 
-  // UdeProblem.recompute: the Recompute<M> view of the model (no stored activations)
-  static constexpr bool RC_VIEW = M::ACT_STORED;
+  // GST weight-gradient GEMM: tile chunks per evaluation (at least one workgroup per CU over the
+  // evaluations) and the backward workspace [G rows | partial slabs [eval][ks][SLAB_TOTAL]]
+  static int gst_ks(int cus, int64_t ne, int n_tiles) {
+    int64_t ks = ne > 0 ? (cus + ne - 1) / ne : 1;
+    if (ks > n_tiles) ks = n_tiles;
+    return ks < 1 ? 1 : (int)ks;
+  }
+  static int64_t gst_rows_floats(int n_tiles, int n_steps) { return (int64_t)n_tiles * n_steps * 4 * TT * M::ACT_A4; }
+
+  // UdeProblem.recompute: the Recompute<M> view of the model (no stored activations; GST needs them)
+  static constexpr bool RC_VIEW = M::ACT_STORED && !M::GST;
   static bool rc(const UdeProblem* p) { return RC_VIEW && p->recompute; }
 
   static int query(const UdeProblem* p, int device, UdeSizes* o) {
@@ -109,9 +122,15 @@ struct Ops {
     o->pack_bytes = M::BAYES ? ne * (int64_t)(M::PACK_TOTAL + M::SLAB_TOTAL) * 4 : (int64_t)M::PACK_TOTAL * 4;
     o->sched_bytes = sched_bytes(p);
     // stage inputs [tile][step][stage][F][16] (+ STORE_ACT / STORE_ACT_D: activations [tile][step][stage][16][ACT_A4])
-    o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::ACT_A4 : 0)) * 4;
+    o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::XST_W : 0)) * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
     o->grad_slab_bytes = (int64_t)gb * M::SLAB_STRIDE * 4 + static_ws_floats(n_tiles) * 4;
+    if constexpr (M::GST) {
+      int cus = 0;
+      HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+      o->grad_slab_bytes = (gst_rows_floats(n_tiles, p->n_steps) +
+                            n_evals(p) * gst_ks(cus, n_evals(p), n_tiles) * (int64_t)M::SLAB_TOTAL) * 4;
+    }
     o->n_params = M::N_GRAD;
     o->grid_fwd = gf;
     o->grid_bwd = gb;
@@ -124,7 +143,7 @@ struct Ops {
     o->dec_pack_bytes = (int64_t)M::DEC_PACK * 4;
     o->ckpt_final_bytes = (int64_t)n_tiles * M::F * TT * 4;
     o->dec_ws_bytes = (int64_t)gd * LossDims<M::R>::SLAB * 4;
-    o->act_bytes = M::ACT_STORED ? (int64_t)n_tiles * p->n_steps * 4 * TT * M::ACT_A4 * 4 : 0;
+    o->act_bytes = M::ACT_STORED ? (int64_t)n_tiles * p->n_steps * 4 * TT * M::XST_W * 4 : 0;
     return UDE_OK;
   }
 
@@ -366,6 +385,29 @@ struct Ops {
 #endif
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
+    if constexpr (M::GST) {
+      // the backward stores the layer-output gradient rows; ude_gst_dw_kernel forms every evaluation's
+      // weight gradient from them and the stored rows, ude_gst_reduce_kernel sums / eps-weights them
+      int cus = 0;
+      HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      const int64_t ne = n_evals(p);
+      const int ks = gst_ks(cus, ne, n_tiles);
+      a.gst = slab;
+      float* part = slab + gst_rows_floats(n_tiles, p->n_steps);
+      hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
+      HIPCHK(hipGetLastError());
+      if (ne > 0) {
+        GstArgs ga;
+        ga.ckpt = ckpt; ga.gst = slab; ga.y0 = y0; ga.part = part;
+        ga.n_traj = p->n_traj; ga.n_steps = p->n_steps; ga.n_tiles = n_tiles; ga.n_ks = ks;
+        hipLaunchKernelGGL((ude_gst_dw_kernel<M>), dim3(ks, (unsigned)ne), dim3(Gst<M>::NT), Gst<M>::LDS, s, ga);
+        HIPCHK(hipGetLastError());
+      }
+      hipLaunchKernelGGL((ude_gst_reduce_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
+                         (const float*)part, (const float*)a.eslab, (int)ne, ks, dparams);
+      HIPCHK(hipGetLastError());
+      return UDE_OK;
+    }
     hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,

@@ -83,6 +83,7 @@ struct KArgs {
   float* yhat;                // DEC forward: (T, N, R) decoder outputs, written instead of the latent
   double* reg_slab;           // DEC forward: per-workgroup latent_init_loss partial sums
   float* ckpt_final;          // DEC training forward: the final-state block (ckpt + ckpt_final_off)
+  float* gst;                 // GST backward: layer-output gradient rows [tile][step][stage][16][ACT_A4]
 };
 
 // latent_init_loss summand (lib/train_functions.py:116-126): |x| where x < 0, |1 - x| where x > 1
@@ -331,14 +332,16 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     constexpr int d = decltype(dd)::value;
     constexpr int NF = M::FQ(W, d);
     // all of this wave's weight fragments (and biases) for the phase are in flight
-    // before its first MFMA
-    f4 fr[(NF > 0 && !RW) ? NF : 1], bias[(M::FT(d) > 0 && !RW) ? M::FT(d) : 1];
+    // before its first MFMA -- unless they would not fit next to the working set (the Bayesian
+    // state model's layer 0, K = 416: 208 VGPRs, spilled at the forward's 256): then chunk by chunk
+    constexpr bool CHUNK_A = !RW && NF > 24;
+    f4 fr[(NF > 0 && !RW && !CHUNK_A) ? NF : 1], bias[(M::FT(d) > 0 && !RW) ? M::FT(d) : 1];
     if constexpr (!RW) {
       sfor<M::FT(d)>([&](auto kk) {
         constexpr int k = decltype(kk)::value;
         if constexpr (M::fowner(d, k) == W) {
           constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
-          load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
+          if constexpr (!CHUNK_A) load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
           if constexpr (M::has_bias(d)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
         }
       });
@@ -371,6 +374,17 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
 #pragma unroll
         for (int q0 = 0; q0 < NQ; q0 += QB) {
           f4 xb[QB];
+          f4 fa[CHUNK_A ? M::FT(d) : 1][CHUNK_A ? QB : 1];
+          if constexpr (CHUNK_A)
+            sfor<M::FT(d)>([&](auto kk) {
+              constexpr int k = decltype(kk)::value;
+              if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net) {
+                constexpr int rt = M::frt(d, k);
+#pragma unroll
+                for (int q = q0; q < q0 + QB && q < NQ; ++q)
+                  fa[k][q - q0] = ldw(rs, lane * 16, (M::wf_off(net, d) + rt * NQ * 256 + q * 256) * 4);
+              }
+            });
 #pragma unroll
           for (int q = q0; q < q0 + QB && q < NQ; ++q) xb[q - q0] = *reinterpret_cast<const f4*>(b + 4 * q);
           __builtin_amdgcn_sched_barrier(0);
@@ -381,9 +395,13 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
             for (int e = 0; e < 4; ++e)
               sfor<M::FT(d)>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
-                if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net)
-                  if constexpr (UDE_ABL != 13) acc[k] = mfma4(FR(M::fq_before(W, d, k) + q)[e], x[e], acc[k]);
+                if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net) {
+                  f4 wq;
+                  if constexpr (CHUNK_A) wq = fa[CHUNK_A ? k : 0][CHUNK_A ? q - q0 : 0];
+                  else wq = FR(M::fq_before(W, d, k) + q);
+                  if constexpr (UDE_ABL != 13) acc[k] = mfma4(wq[e], x[e], acc[k]);
                   else acc[k][e] += x[e];
+                }
               });
           }
         }
@@ -451,17 +469,26 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
 // checkpoints and stored activations (the decoder backward reads every output state from there).
 template <class M>
 __host__ __device__ __forceinline__ size_t ckpt_final_off(int n_tiles, int n_steps) {
-  return (size_t)n_tiles * n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::ACT_A4 : 0));
+  return (size_t)n_tiles * n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::XST_W : 0));
 }
 
-// Stored activations (Model::STORE_ACT) of one tile-stage: [16][ACT_A4] behind the checkpoint.
+// Stored activations (Model::ACT_STORED) of one tile-stage: [16][XST_W] behind the checkpoint.
 template <class M>
-__device__ __forceinline__ float* act_block(float* ckpt, int n_tiles, int n_steps, int tile, int step, int stage) {
+__host__ __device__ __forceinline__ float* act_block(float* ckpt, int n_tiles, int n_steps, int tile, int step,
+                                                     int stage) {
   const size_t ck = (size_t)n_tiles * n_steps * 4 * M::F * TT;
-  return ckpt + ck + (((size_t)tile * n_steps + step) * 4 + stage) * TT * M::ACT_A4;
+  return ckpt + ck + (((size_t)tile * n_steps + step) * 4 + stage) * TT * M::XST_W;
 }
 template <class M>
 constexpr int act_q_per_thread() { return (TT * M::ACT_A4 / 4 + NTHREADS - 1) / NTHREADS; }
+// Quad i of a tile-stage's activation rows ([16][ACT_A4] in record order, i = t * ACT_A4 / 4 + q)
+// -> its quad index in the stored block ([16][XST_W], activation rows at column ACT_IN).
+template <class M>
+__host__ __device__ __forceinline__ int act_src_q(int i) {
+  constexpr int QR = M::ACT_A4 / 4;
+  if constexpr (M::XST_W == M::ACT_A4) return i;
+  else return (i / QR) * (M::XST_W / 4) + M::ACT_IN / 4 + (i - (i / QR) * QR);
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -589,7 +616,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
               const int i = tid + (u0 + uu) * NTHREADS;
               if (u0 + uu < NQ && i < TT * QR) {
                 const int t = i / QR, q = i - t * QR;
-                dst[i] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+                dst[act_src_q<M>(i)] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
               }
             }
           }
@@ -605,6 +632,15 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             float Y[3], f[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) Y[c] = rec[M::Y_OFF + 3 * r + c];
+            if constexpr (TRAIN && M::GST) {
+              // the stage input in front of the stored activation rows (the layer-0 input of the
+              // weight-gradient GEMM); its pad columns [F, F16) zeroed by the last region's threads
+              float* xrow = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j) + t * M::XST_W;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) xrow[3 * r + c] = Y[c];
+              if (r == M::R - 1)
+                for (int c = M::F; c < M::F16; ++c) xrow[c] = 0.f;
+            }
             if constexpr (M::HAS_P) {
               const float q0 = rec[M::act_off(0, M::nl(0) - 1) + 2 * r];
               const float q1 = rec[M::act_off(0, M::nl(0) - 1) + 2 * r + 1];
@@ -745,7 +781,7 @@ __device__ void fwd_sbody(const KArgs& A, float* lds) {
 #pragma unroll
         for (int u = 0; u < NQ; ++u) {
           const int i = wt + u * NTHREADS;
-          if (i < TT * QR) dst[i] = v[u];
+          if (i < TT * QR) dst[act_src_q<M>(i)] = v[u];
         }
         lds_sync();                            // flux pass (the next stage rewrites the rows)
       }
@@ -821,9 +857,11 @@ struct RkAdjointEp {
 // bias row sums into DBS): d|std| = sum_eval eps_eval * dW_eval (models_bayes.py:45-46).
 // DX_ONLY (SPLIT_BWD critical-path waves): only the input gradients; the weight gradients of
 // the phase are the partner waves' (mlp_backward_dw).
+// GST: the wave's owned rows of every layer-output gradient also go to `gblk` (this tile-stage's
+// [16][ACT_A4] block, record column order) for ude_gst_dw_kernel.
 template <class M, int W, int SR, bool DX_ONLY = false, class DW, class DS, class G0, class EP0, class WR>
 __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
-                                             Prof* pf, const EP0& ep0, const WR& wr) {
+                                             Prof* pf, const EP0& ep0, const WR& wr, float* gblk = nullptr) {
   constexpr bool RW = WR::ON;
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
@@ -838,9 +876,9 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       else return fx[i];
     };
     // BAYES: this evaluation's eps for the wave's dW tiles (C layout) and bias rows
-    constexpr int NE = M::BAYES ? M::ndw_phase(W, d) : 0;
+    constexpr int NE = (M::BAYES && !DX_ONLY) ? M::ndw_phase(W, d) : 0;
     f4 ef[NE > 0 ? NE : 1], eb[M::FT(d) > 0 ? M::FT(d) : 1];
-    if constexpr (M::BAYES) {
+    if constexpr (M::BAYES && !DX_ONLY) {
       sfor<M::FT(d)>([&](auto kk) {
         constexpr int k = decltype(kk)::value;
         if constexpr (M::fowner(d, k) == W) {
@@ -983,6 +1021,16 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         __builtin_amdgcn_sched_barrier(0);
       }
     });
+    if constexpr (M::GST) {
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          constexpr int net = M::fnet(d, k), rt = M::frt(d, k);
+          const f4 gv = *reinterpret_cast<const f4*>(rec + M::gbuf(net, d) + rt * 16 + g * 4);
+          *reinterpret_cast<f4*>(gblk + t * M::ACT_A4 + (M::act_off(net, d) - M::ACT0) + rt * 16 + g * 4) = gv;
+        }
+      });
+    }
     // (2) gradient w.r.t. the layer input (rows = input features); tiles sharing a
     // B operand (the same net's output gradient) are interleaved
     f4 xa[M::XT(d) > 0 ? M::XT(d) : 1];
@@ -1437,10 +1485,12 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   }
 
   // SPLITB: the weight-gradient accumulators live on the partner waves (bwd_wbody / bwd_wbody_l)
-  f4 dw[M::SPLITB ? 1 : NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], c1[NZn];
+  // GST: no weight-gradient accumulators (ude_gst_dw_kernel forms them from the stored rows)
+  constexpr bool NO_DW = M::SPLITB || M::GST;
+  f4 dw[NO_DW ? 1 : NDWn], dws[(M::BAYES && !M::GST) ? NDWn : 1], g0t[NZn], c1[NZn];
 #pragma unroll
-  for (int i = 0; i < (M::SPLITB ? 1 : NDWn); ++i) dw[i] = f4zero();
-  if constexpr (M::BAYES) {
+  for (int i = 0; i < (NO_DW ? 1 : NDWn); ++i) dw[i] = f4zero();
+  if constexpr (M::BAYES && !M::GST) {
 #pragma unroll
     for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
   }
@@ -1465,7 +1515,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     // the record's static features feed only the static hoist of a recomputed forward (and FULL0's
     // layer 0); with stored activations their alias of the activation region must stay untouched
     // (the SPLIT_BWD_L partner waves fill it by LDS-DMA meanwhile)
-    if constexpr (!M::ACT_STORED || M::FULL0) load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
+    if constexpr (!M::ACT_STORED || (M::FULL0 && !M::GST)) load_static<M, SR, M::XSB_OFF>(A.y0, lds, n0, A.n_traj);
     if constexpr (M::FULL0) {
       #pragma unroll 1
       for (int i = tid; i < TT * M::S16; i += NTHREADS) {
@@ -1519,6 +1569,8 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     // CARRY: the next step's output cotangents are loaded at stage 1 of the step (a whole stage
     // ahead of the flux pass of stage 0 that consumes them)
     float gvc[SL][3];
+    // GST: the next stage's checkpointed input is carried in registers (no LDS staging slot)
+    float ckg[M::GST ? SL : 1][3];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's
@@ -1561,7 +1613,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 #pragma unroll
           for (int u = 0; u < act_q_per_thread<M>(); ++u) {
             const int i = tid + u * NTHREADS;
-            if (i < TT * QR) av[u] = src[i];
+            if (i < TT * QR) av[u] = src[act_src_q<M>(i)];
           }
 #pragma unroll
           for (int u = 0; u < act_q_per_thread<M>(); ++u) {
@@ -1591,6 +1643,16 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = ckr[0][c];
           }
+        } else if (M::GST && have_next) {
+          sfor<SL>([&](auto ss) {
+            constexpr int sl = decltype(ss)::value;
+            const int p = tid + sl * NTHREADS;
+            if (p < M::PAIRS) {
+              const int r = p / TT, t = p - r * TT;
+#pragma unroll
+              for (int c = 0; c < 3; ++c) lds[t * SR + M::Y_OFF + 3 * r + c] = ckg[M::GST ? sl : 0][c];
+            }
+          });
         } else if (have_next) {
           // the 3R stage-input features (quads of the F4-wide staging row, clipped to the
           // record's F16-wide Y slot: beyond it starts the activation region)
@@ -1623,7 +1685,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
               const int i = tid + u * NTHREADS;
               if (i < TT * QR) {
                 const int t = i / QR, q = i - t * QR;
-                *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = src[i];
+                *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = src[act_src_q<M>(i)];
               }
             }
           }
@@ -1675,7 +1737,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
 #pragma unroll
             for (int u = 0; u < act_q_per_thread<M>(); ++u) {
               const int i = tid + u * NTHREADS;
-              if (i < TT * QR) actr[u] = src[i];
+              if (i < TT * QR) actr[u] = src[act_src_q<M>(i)];
             }
           }
           if constexpr (UDE_ABL != 2) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
@@ -1695,7 +1757,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
             #pragma unroll
             for (int u = 0; u < act_q_per_thread<M>(); ++u) {
               const int i = tid + u * NTHREADS;
-              if (i < TT * QR) actn[u] = src[i];
+              if (i < TT * QR) actn[u] = src[act_src_q<M>(i)];
             }
           }
           if (next_out) out_issue<M>(A, sc, nstep, n0, gvn);
@@ -1740,7 +1802,12 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 17);
-        if (!CARRY && !M::SPLIT_BWD_L && have_next) {
+        if (M::GST && !CARRY && have_next) {
+#pragma unroll
+          for (int sl = 0; sl < (M::GST ? SL : 1); ++sl)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) ckg[sl][c] = ckn[sl][c];
+        } else if (!CARRY && !M::SPLIT_BWD_L && have_next) {
           sfor<SL>([&](auto ss) {
             constexpr int sl = decltype(ss)::value;
             const int p = tid + sl * NTHREADS;
@@ -1756,8 +1823,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         lds_sync();
         UDE_STAMP(pf, 11);
         if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { lds_sync(); });
-        else mlp_backward<M, W, SR, M::SPLITB>(rse, es, lds, dw, dws, g0t, lane, pf,
-                                             RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr);
+        else mlp_backward<M, W, SR, NO_DW>(rse, es, lds, dw, dws, g0t, lane, pf,
+                                           RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr,
+                                           M::GST ? A.gst + (((size_t)tile * A.n_steps + step) * 4 + jj) * TT * M::ACT_A4
+                                                  : nullptr);
         if constexpr (M::SPLITX0) {
           // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
           // use the step-end thread <-> (t, quad) mapping, so the step end needs no barrier.
@@ -1844,11 +1913,11 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   }
 
   // ---- kernel end: register tiles + LDS row sums -> this workgroup's slab ----
-  if constexpr (!M::SPLITB) dw_to_slab<M, W>(dw, dws, myslab, lane);
+  if constexpr (!NO_DW) dw_to_slab<M, W>(dw, dws, myslab, lane);
   // SPLITB: the partner waves' last bias row sums land before this barrier
   if constexpr (M::SPLITB) lds_sync();
   #pragma unroll 1
-  for (int i = tid; i < M::NDB; i += NTHREADS) {
+  for (int i = tid; i < (M::GST ? 0 : M::NDB); i += NTHREADS) {
     myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
     if constexpr (M::BAYES) myslab[M::SLAB_TOTAL + M::SLAB_DB + i] = lds[M::DBS_LDS + i];
   }
@@ -1904,7 +1973,7 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
 #pragma unroll
     for (int u = 0; u < NQ; ++u) {
       const int i = wt + u * NTHREADS;
-      if (i < TT * QR) actr[u] = src[i];
+      if (i < TT * QR) actr[u] = src[act_src_q<M>(i)];
     }
   };
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
@@ -2009,13 +2078,13 @@ __device__ __forceinline__ void dma_layer(Rsrc src, float* lds, int lane) {
 #if defined(__HIP_DEVICE_COMPILE__)
     if (lane < KO / 4)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (LdsPtr)(lds + t * SR + OFF), 16, 16 * lane,
-                                               (t * M::ACT_A4 + (OFF - M::ACT0)) * 4, 0, 0);
+                                               (t * M::XST_W + M::ACT_IN + (OFF - M::ACT0)) * 4, 0, 0);
 #endif
   }
 }
 template <class M>
 __device__ __forceinline__ Rsrc act_rsrc(const KArgs& A, int tile, int step, int jj) {
-  return make_rsrc(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj), TT * M::ACT_A4 * 4);
+  return make_rsrc(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, jj), TT * M::XST_W * 4);
 }
 // the layers whose last reader of the current stage is phase d (d = D: the flux pass)
 template <class M, int W, int d>

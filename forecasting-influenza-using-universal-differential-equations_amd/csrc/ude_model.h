@@ -86,6 +86,31 @@ struct Model {
     return (FTbase(d) + FT(d) + m) % WAVES;
   }
 
+  // ---- per-wave register tiles -----------------------------------------------------
+  static constexpr int ndw_before(int w, int d, int k) {
+    int s = 0;
+    for (int e = 0; e < D; ++e)
+      for (int kk = 0; kk < FT(e); ++kk) {
+        if (e == d && kk == k) return s;
+        if (fowner(e, kk) == w) s += rti(fnet(e, kk), e);
+      }
+    return s;
+  }
+  static constexpr int NDW(int w) { return ndw_before(w, D, 0); }
+  // dW tiles wave w accumulates in phase (layer) d
+  static constexpr int ndw_phase(int w, int d) {
+    int s = 0;
+    for (int kk = 0; kk < FT(d); ++kk)
+      if (fowner(d, kk) == w) s += rti(fnet(d, kk), d);
+    return s;
+  }
+  static constexpr int max_ndw() { return cmax(cmax(NDW(0), NDW(1)), cmax(NDW(2), NDW(3))); }
+  // BAYES keeps a second (eps-weighted) accumulator per dW tile in registers when both sets fit
+  // (R = 1 at the reference's sizes).  Larger Bayesian models (GST) store each evaluation's
+  // layer-output gradient rows instead and a separate kernel (ude_gst_dw_kernel) forms every
+  // evaluation's weight gradient as one GEMM over the whole batch, eps-weighting it there.
+  static constexpr bool GST = BAYES && max_ndw() > 20;
+  static constexpr bool FITS = true;
   // ---- LDS record: one row of SR floats per trajectory ([t][feature]) ---------
   static constexpr int Y_OFF = 0;
   // FULL0: the static features sit right after the dynamic ones for the whole tile
@@ -110,7 +135,12 @@ struct Model {
     for (int j = 0; j < nl(net); ++j) m = cmax(m, kout(net, j));
     return m;
   }
+  // GST (no weight gradients in the backward): the backward never reads the record's static features,
+  // so the rate net's two gradient buffers live in their columns when they fit (R = 49: the record
+  // then fits the LDS)
+  static constexpr bool GB_IN_STATIC = GST && 2 * gbs(0) <= S16;
   static constexpr int gb_off(int net, int parity) {
+    if (GB_IN_STATIC) return net == 0 ? F16 + parity * gbs(0) : ALIAS_END + parity * gbs(1);
     return ALIAS_END + (net == 0 ? 0 : 2 * gbs(0)) + parity * gbs(net);
   }
   static constexpr int gbuf(int net, int i) { return gb_off(net, i & 1); }
@@ -123,7 +153,7 @@ struct Model {
   // quads of the RK-state rows holding live features (3R of them; the rest stay zero): the
   // per-(trajectory, quad) RK passes of the backward touch only these
   static constexpr int NVL = (3 * R + 3) / 4;
-  static constexpr int RK_A = ALIAS_END + 2 * gbs(0) + 2 * gbs(1);  // adjoint of y_{n+1} (carried across steps)
+  static constexpr int RK_A = ALIAS_END + (GB_IN_STATIC ? 0 : 2 * gbs(0)) + 2 * gbs(1);  // adjoint of y_{n+1}
   static constexpr int RK_PEND = RK_A + F4;       // y_n-side share of interpolated outputs
   static constexpr int RK_ACCY = RK_PEND + F4;    // adjoint of y_n being accumulated
   static constexpr int RK_DK1 = RK_ACCY + F4;
@@ -146,9 +176,10 @@ struct Model {
   static constexpr int DBS_LDS = DB_LDS + NDB;
   // + staging slot for the next stage's checkpointed input ([t][F4], prefetched
   // during the flux pass)
-  static constexpr int STG_LDS = DB_LDS + (BAYES ? 2 : 1) * NDB;
+  // (GST: no bias row sums, and the next stage's input is carried in registers: no staging slot)
+  static constexpr int STG_LDS = DB_LDS + (GST ? 0 : (BAYES ? 2 : 1) * NDB);
   // SPLITX0: per-wave partial layer-0 input-gradient tiles [WAVES][XT(0)][64 lanes][4]
-  static constexpr int X0P_LDS = STG_LDS + TT * F4;
+  static constexpr int X0P_LDS = STG_LDS + (GST ? 0 : TT * F4);
   // ---- stored activations (small models) ----------------------------------------------
   // At one tile per CU the backward's per-stage recompute of the forward (4 layer phases, each
   // a barrier-separated latency chain) costs more than streaming the activations through HBM:
@@ -164,7 +195,7 @@ struct Model {
   // start (STORE_ACT_D): one exposed HBM latency per stage instead of the recompute's four
   // barrier-separated layer phases (a third of the backward's MFMA work).  1.5 GB for the
   // 20,480-trajectory x 8-step state49 solve.
-  static constexpr bool STORE_ACT_D = !STORE_ACT && !BAYES;
+  static constexpr bool STORE_ACT_D = !STORE_ACT && (!BAYES || GST);
   static constexpr bool ACT_STORED = STORE_ACT || STORE_ACT_D;
   // Two waves per SIMD in the backward of small deterministic records (SPLIT_BWD): at one tile
   // per CU a single wave per SIMD leaves every LDS latency, epilogue and barrier of a stage's
@@ -188,7 +219,13 @@ struct Model {
   // Training forward of small records at one tile per CU: four more waves copy each stage's
   // activation rows from the record to HBM during the flux pass, off the critical path
   // (ude_kernels.h fwd_sbody).  With more tiles than CUs two 4-wave workgroups per CU win.
-  static constexpr bool SPLIT_FWD = STORE_ACT && SLOTS_ == 1;
+  static constexpr bool SPLIT_FWD = STORE_ACT && SLOTS_ == 1 && !GST;
+  // Stored row layout ([tile][step][stage][16][XST_W] behind the checkpoint): the activation rows
+  // [ACT0, ACT_END) of the record at column ACT_IN.  GST rows also carry the stage input [0, F16)
+  // in front (written by the flux pass before it overwrites the Y slot): the weight-gradient GEMM
+  // multiplies the layer-0 output gradients by [stage input | static features] per evaluation.
+  static constexpr int ACT_IN = GST ? F16 : 0;
+  static constexpr int XST_W = ACT_IN + ACT_A4;
   static constexpr int ACT_STG = X0P_LDS + (XT(0) < WAVES ? WAVES * XT(0) * 256 : 0);
   static constexpr int LDS_B = (ACT_STG + (STORE_ACT ? TT * ACT_A4 : 0)) * 4;
   static_assert(LDS_F <= 160 * 1024 && LDS_B <= 160 * 1024, "record does not fit the 160 KiB LDS");
@@ -245,28 +282,6 @@ struct Model {
   static constexpr int STATIC_CHUNKS = 128;
   static constexpr int STATIC_GROUPS = (S16 / 16 + 3) / 4;
 
-  // ---- per-wave register tiles -----------------------------------------------------
-  static constexpr int ndw_before(int w, int d, int k) {
-    int s = 0;
-    for (int e = 0; e < D; ++e)
-      for (int kk = 0; kk < FT(e); ++kk) {
-        if (e == d && kk == k) return s;
-        if (fowner(e, kk) == w) s += rti(fnet(e, kk), e);
-      }
-    return s;
-  }
-  static constexpr int NDW(int w) { return ndw_before(w, D, 0); }
-  // dW tiles wave w accumulates in phase (layer) d
-  static constexpr int ndw_phase(int w, int d) {
-    int s = 0;
-    for (int kk = 0; kk < FT(d); ++kk)
-      if (fowner(d, kk) == w) s += rti(fnet(d, kk), d);
-    return s;
-  }
-  static constexpr int max_ndw() { return cmax(cmax(NDW(0), NDW(1)), cmax(NDW(2), NDW(3))); }
-  // BAYES keeps a second (eps-weighted) accumulator per dW tile in registers; larger
-  // models are not compiled in (ude_supported() reports them as unsupported)
-  static constexpr bool FITS = !BAYES || max_ndw() <= 20;
   static constexpr int ng_before(int w, int d, int k) {
     int s = 0;
     for (int e = 0; e < D; ++e)

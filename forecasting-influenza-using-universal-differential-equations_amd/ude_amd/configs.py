@@ -48,6 +48,12 @@ PREBUILT += [
     _c("BFaFp", 1, 8, [64, 64, 32], [64, 64]),
     _c("BFp", 1, 8, [64, 64, 32], None),
     _c("BFa", 1, 8, None, [64, 64]),
+    # ... and the hhs / state region sets (R = 10, 49): whole-solve kernels with the weight gradients
+    # formed per evaluation by ude_gst_dw_kernel (Model::GST)
+    _c("BFaFp", 10, 8, [64, 64, 32], [64, 64]),
+    _c("BFp", 10, 8, [64, 64, 32], None),
+    _c("BFaFp", 49, 8, [64, 64, 32], [64, 64]),
+    _c("BFp", 49, 8, [64, 64, 32], None),
     _c("BFaFp", 1, 8, [20, 20], [32, 32]),           # models_bayes.py class defaults
     _c("BFp", 1, 8, [20, 20], None),
     _c("BFa", 1, 8, None, [32, 32]),

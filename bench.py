@@ -59,6 +59,9 @@ WORKLOADS = {
     "bayes_us": dict(_US, kind="Bayes_FaFp", n_traj=4096, t=("arange", 366, 7.0),
                      desc="Bayesian US model (models_bayes.py Bayes_FaFp, fresh weight sample per RHS "
                           "evaluation), R=1, 4096 trajectories x 365 daily RK4 steps"),
+    "bayes_state49": dict(_STATE, kind="Bayes_FaFp", n_traj=64 * 10 * 32, t=("arange", 9, 1.0),
+                          desc="Bayesian state model (models_bayes.py Bayes_FaFp, run_ode.py 'UONNb'), R=49, "
+                               "64 MC samples x 10 seasons x 32 windows, 8 weekly RK4 steps"),
     "tiny": dict(_US, n_traj=64, t=("arange", 5, 1.0),
                  desc="plumbing rehearsal only (CPU / gloo): US model, 64 trajectories, 4 weekly steps"),
 }
@@ -336,14 +339,15 @@ def adjoint_line(pkg, w, dev, T=2, rtol=1e-5, atol=1e-7, seminorm=True, reps=2):
 
 def bayes_large_line(pkg, dev, steps=3):
     """SURVEY 8f row 1 at the state model's size: Bayes_FaFp R=49 (run_ode.py 'UONNb'), 20,480
-    trajectories x 8 weekly RK4 steps, fwd+bwd; each RHS evaluation draws its weight sample and
-    runs on the gfx950 evaluation + VJP kernels (the whole-solve kernel's two register dW sets
-    do not fit this size)."""
+    trajectories x 8 weekly RK4 steps, fwd+bwd; every RHS evaluation draws its own weight sample
+    (models_bayes.py:43-48).  Whole-solve kernels (Model::GST): the training forward stores each
+    stage's layer inputs, the backward the layer-output gradients, and ude_gst_dw_kernel forms every
+    evaluation's weight gradient as one GEMM over the batch, eps-weighted by a fixed-order reduce."""
     w = dict(WORKLOADS["state49"], kind="Bayes_FaFp")
     mod, y0, t, dlat = build(pkg, w, dev, seed=21)
     el, k = time_steps(pkg, None, mod, y0, t, dlat, 1, steps, 1, lambda: None, dev)
     v = w["n_traj"] * (len(t) - 1) * steps / el
-    return {"workload": "Bayes_FaFp R=49, 20480 trajectories x 8 weekly RK4 steps (per-evaluation kernels)",
+    return {"workload": "Bayes_FaFp R=49, 20480 trajectories x 8 weekly RK4 steps (whole-solve GST kernels)",
             "traj_steps_per_s": v, "ms_per_step": el / steps * 1e3}
 
 

@@ -123,6 +123,8 @@ struct Ops {
     o->sched_bytes = sched_bytes(p);
     // stage inputs [tile][step][stage][F][16] (+ STORE_ACT / STORE_ACT_D: activations [tile][step][stage][16][ACT_A4])
     o->ckpt_bytes = (int64_t)n_tiles * p->n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::XST_W : 0)) * 4;
+    // GST: + the tiles' static features [tile][16][S16] (the weight-gradient GEMM's layer-0 input)
+    if (M::GST) o->ckpt_bytes += (int64_t)n_tiles * TT * M::S16 * 4;
     o->stats_slab_bytes = (int64_t)gf * 5 * 8;
     o->grad_slab_bytes = (int64_t)gb * M::SLAB_STRIDE * 4 + static_ws_floats(n_tiles) * 4;
     if constexpr (M::GST) {
@@ -704,6 +706,17 @@ struct EvalOps {
   }
   static int vjp(const UdeProblem* p, const float* pack, const float* x, const float* cot_f, const float* cot_rates,
                  const float* cot_fa, float* dx, void* ws, float* dparams, hipStream_t s) {
+    return eval_vjp(p, pack, x, cot_f, cot_rates, cot_fa, nullptr, 1.f, dx, ws, dparams, s);
+  }
+  // odeint_adjoint's augmented evaluation: f (scaled) and the VJP in one launch
+  static int fused(const UdeProblem* p, const float* pack, const float* x, const float* cot_f, float* fout,
+                   float f_scale, float* dx, void* ws, float* dparams, hipStream_t s) {
+    if (!fout) return UDE_E_INVALID;
+    return eval_vjp(p, pack, x, cot_f, nullptr, nullptr, fout, f_scale, dx, ws, dparams, s);
+  }
+  static int eval_vjp(const UdeProblem* p, const float* pack, const float* x, const float* cot_f,
+                      const float* cot_rates, const float* cot_fa, float* fout, float f_scale, float* dx, void* ws,
+                      float* dparams, hipStream_t s) {
     if constexpr (M::BAYES) {
       return UDE_E_UNSUPPORTED;
     } else {
@@ -722,6 +735,7 @@ struct EvalOps {
     a.pack = pack; a.x = x; a.cot_f = cot_f; a.cot_rates = cot_rates; a.cot_fa = cot_fa;
     a.dx = dx; a.slab = slab; a.g0buf = g0buf;
     a.n_traj = p->n_traj; a.n_tiles = n_tiles; a.fa_w = p->fa_w;
+    a.fout = fout; a.f_scale = f_scale;
     hipLaunchKernelGGL((ude_eval_vjp_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
@@ -774,6 +788,8 @@ struct Entry {
   int (*nll_workspace)(int, int, int, int64_t*);
   int (*nll_forward)(int, int, int, const float*, const float*, void*, float*, hipStream_t);
   int (*nll_backward)(int, int, int, const float*, const float*, const float*, const void*, float*, hipStream_t);
+  int (*rhs_eval_vjp)(const UdeProblem*, const float*, const float*, const float*, float*, float, float*, void*,
+                      float*, hipStream_t);
 };
 
 template <class M>
@@ -782,7 +798,7 @@ constexpr Entry make_entry() {
                &DopriOps<M>::workspace, &DopriOps<M>::forward, &LossOps<M>::workspace, &LossOps<M>::forward,
                &LossOps<M>::backward, &LossOps<M>::backward_sir, &EvalOps<M>::workspace, &EvalOps<M>::forward,
                &EvalOps<M>::vjp, &Ops<M>::dec_pack, &Ops<M>::forward_dec, &Ops<M>::dec_backward,
-               &Ops<M>::nll_workspace, &Ops<M>::nll_forward, &Ops<M>::nll_backward};
+               &Ops<M>::nll_workspace, &Ops<M>::nll_forward, &Ops<M>::nll_backward, &EvalOps<M>::fused};
 }
 
 

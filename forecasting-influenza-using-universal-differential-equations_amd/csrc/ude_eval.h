@@ -31,7 +31,43 @@ struct EArgs {
   float* g0buf;            // VJP: per-trajectory layer-0 output gradients [tile][K0][16] (HOIST)
   int n_traj, n_tiles;
   float fa_w;
+  float* fout;             // VJP (nullable): f_scale * f(x) (N, R, L) from the same launch
+  float f_scale;
 };
+
+// f = RHS(x) of pair p from the record after mlp_forward (lib/models.py:130-150), scaled by `scale`
+// (dims >= 3 zero, masked outside [-1, 2]).
+template <class M, int SR>
+__device__ __forceinline__ void eval_f_pairs(const float* lds, const EArgs& A, int n0, float* out, float scale) {
+  #pragma unroll 1
+  for (int p = threadIdx.x; p < M::PAIRS; p += NTHREADS) {
+    const int r = p / TT, t = p - r * TT, n = n0 + t;
+    if (n >= A.n_traj) continue;
+    const float* rec = lds + t * SR;
+    float Y[3], f[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Y[c] = rec[M::Y_OFF + 3 * r + c];
+    if constexpr (M::HAS_P) {
+      const float b = fabsf(rec[M::act_off(0, M::nl(0) - 1) + 2 * r]);
+      const float gm = fabsf(rec[M::act_off(0, M::nl(0) - 1) + 2 * r + 1]);
+      const float plus = (b * Y[0]) * Y[1];
+      const float minus = gm * Y[1];
+      f[0] = -plus; f[1] = plus - minus; f[2] = minus;
+    }
+    if constexpr (M::HAS_A) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v = rec[M::act_off(1, M::nl(1) - 1) + 3 * r + c];
+        if constexpr (M::HAS_P) f[c] = f[c] + A.fa_w * v;
+        else f[c] = v;
+      }
+    }
+    float* dst = out + ((size_t)n * M::R + r) * M::L;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dst[c] = scale * ((Y[c] > 2.f || Y[c] < -1.f) ? 0.f : f[c]);
+    for (int c = 3; c < M::L; ++c) dst[c] = 0.f;
+  }
+}
 
 // ---- forward --------------------------------------------------------------------------
 template <class M, int W>
@@ -226,6 +262,7 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     __syncthreads();
     mlp_forward<M, W, SR>(rs, lds, c1, lane, wr);
+    if (A.fout) eval_f_pairs<M, SR>(lds, A, n0, A.fout, A.f_scale);
     eval_flux_backward<M, SR>(lds, A, n0);
     // zero the padded rows of the final-layer gradient slots
     if constexpr (M::HAS_P) {

@@ -14,11 +14,11 @@
 //    of the evaluation belongs to one wave (whole row tiles, balanced greedily over the waves) and is
 //    accumulated in registers over the chunk, then written once to the partial slab [e][ks] (the
 //    backward slab layout: dW tiles in MFMA C order, then the bias rows = trajectory sums of G);
-//  * half-tiles of 8 trajectories are double-buffered in LDS ([t][Y | static | activations | G] rows,
-//    the backward record's column order, row stride = 4 mod 64): the next half-tile's rows arrive by
-//    LDS-DMA (buffer loads with the LDS destination, no data registers) and its static features
-//    (latent dims >= 3 of y0, per-trajectory constants) through registers, while the waves multiply
-//    the current one (v_mfma_f32_16x16x4_f32, MFMA step s over trajectories 4 s + lane group);
+//  * half-tiles of 8 trajectories are triple-buffered in LDS ([t][Y | static | activations | G] rows,
+//    the backward record's column order, row stride = 4 mod 64): the next two half-tiles' rows arrive
+//    by LDS-DMA (buffer loads with the LDS destination, no data registers; the static features from
+//    the per-tile block the training forward wrote) while the waves multiply the current one
+//    (v_mfma_f32_16x16x4_f32, MFMA step s over trajectories 4 s + lane group);
 //  * ude_gst_reduce_kernel sums the chunks in fixed order per evaluation, weights each evaluation's
 //    sum by its eps (slab order, ude_eps_slab_kernel) and scatters d mean / d |std| to torch order.
 // Bandwidth-balanced at R = 49: ~98 KB of rows per 16 trajectories and evaluation against 1208
@@ -35,7 +35,9 @@ struct Gst {
   static constexpr int SRG = M::stride(GOFF + M::ACT_A4);
   static constexpr int HT = 8;                               // trajectories per half-tile
   static constexpr int BUF = HT * SRG;                       // floats per LDS buffer
-  static constexpr int LDS = 2 * BUF * 4;
+  // three buffers when they fit (two half-tiles in flight while one is multiplied), else two
+  static constexpr int NBUF = 3 * BUF * 4 <= 160 * 1024 ? 3 : 2;
+  static constexpr int LDS = NBUF * BUF * 4;
   static_assert(LDS <= 160 * 1024, "GST half-tile buffers do not fit the 160 KiB LDS");
   // row tiles r = FTbase(d) + k of every layer, in slab order
   static constexpr int NRT = M::FTbase(M::D);
@@ -74,15 +76,29 @@ struct Gst {
   static constexpr int rows_before(int, int r) { return TAB.row[r]; }
   static constexpr int NACC(int w) { return TAB.nacc[w]; }
   static constexpr int NROW(int w) { return TAB.nrow[w]; }
-  // LDS-DMA jobs of one half-tile: per row, the stage input (F16 floats), the activation rows and
-  // the output-gradient rows (ACT_A4 each), up to 256 floats (64 lanes x 16 B) per job
-  static constexpr int NJY = (M::F16 + 255) / 256, NJA = (M::ACT_A4 + 255) / 256;
-  static constexpr int NJR = NJY + 2 * NJA;
+  // LDS-DMA jobs of one half-tile: per row, the stage input (F16 floats), the static features (S16,
+  // the tile's block the training forward wrote), the activation rows and the output-gradient rows
+  // (ACT_A4 each), up to 256 floats (64 lanes x 16 B) per job
+  static constexpr int NJY = (M::F16 + 255) / 256, NJS = (M::S16 + 255) / 256, NJA = (M::ACT_A4 + 255) / 256;
+  static constexpr int NJR = NJY + NJS + 2 * NJA;
   static constexpr int NJ = HT * NJR;
-  // static-feature gathers per thread (scalar loads of y0 rows, latent dims >= 3 kept)
-  static constexpr int RL = M::R * M::L;
-  static constexpr int NSV = (HT * RL + NT - 1) / NT;
+  // LDS-DMA instructions wave w issues per half-tile
+  static constexpr int ndma(int w) {
+    int s = 0;
+    for (int j = 0; j < NJ; ++j)
+      if (j % NW == w) s += 1;
+    return s;
+  }
 };
+
+// s_waitcnt vmcnt(n) (expcnt / lgkmcnt untouched)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt out of range");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 struct GstArgs {
   const float* ckpt;     // training store (stage inputs + [16][XST_W] stored rows)
@@ -110,74 +126,57 @@ __device__ void gst_body(const GstArgs& A, float* lds) {
 #pragma unroll
   for (int i = 0; i < NB; ++i) bacc[i] = 0.f;
 
-  // both buffers zeroed once: the static pads [F16 + S, F16 + S16) are never written
+  // the buffers zeroed once: the static pads [F16 + S, F16 + S16) are never written
   #pragma unroll 1
-  for (int i = tid; i < 2 * P::BUF; i += P::NT) lds[i] = 0.f;
+  for (int i = tid; i < P::NBUF * P::BUF; i += P::NT) lds[i] = 0.f;
   lds_sync();
+  auto bufp = [&](int h) { return lds + (h % P::NBUF) * P::BUF; };
 
-  auto issue = [&](int h) {                     // LDS-DMA of half-tile h's rows into buffer h & 1
+  auto issue = [&](int h) {                     // LDS-DMA of half-tile h's rows into its buffer
     const int tile = h >> 1, r0 = (h & 1) * HT;
-    float* buf = lds + (h & 1) * P::BUF;
+    float* buf = bufp(h);
     const Rsrc xs = make_rsrc(act_block<M>(const_cast<float*>(A.ckpt), A.n_tiles, A.n_steps, tile, step, jj),
                               TT * M::XST_W * 4);
     const Rsrc gs = make_rsrc(A.gst + (((size_t)tile * A.n_steps + step) * 4 + jj) * TT * M::ACT_A4,
                               TT * M::ACT_A4 * 4);
+    const Rsrc ss = make_rsrc(A.ckpt + ckpt_final_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16,
+                              TT * M::S16 * 4);
     sfor<P::NJ>([&](auto jb) {
       constexpr int j = decltype(jb)::value;
       if constexpr (j % P::NW == W) {
         constexpr int row = j / P::NJR, sj = j % P::NJR;
-        constexpr bool isY = sj < P::NJY, isA = !isY && sj < P::NJY + P::NJA;
-        constexpr int c = isY ? sj : (isA ? sj - P::NJY : sj - P::NJY - P::NJA);   // 256-float chunk
-        constexpr int segw = isY ? M::F16 : M::ACT_A4;
+        // kind: 0 stage input, 1 static features, 2 activation rows, 3 output-gradient rows
+        constexpr int kind = sj < P::NJY ? 0 : sj < P::NJY + P::NJS ? 1 : sj < P::NJY + P::NJS + P::NJA ? 2 : 3;
+        constexpr int c = kind == 0 ? sj : kind == 1 ? sj - P::NJY : kind == 2 ? sj - P::NJY - P::NJS
+                                                                                : sj - P::NJY - P::NJS - P::NJA;
+        constexpr int segw = kind == 0 ? M::F16 : kind == 1 ? M::S16 : M::ACT_A4;
         constexpr int nq = cmin(64, (segw - 256 * c) / 4);                        // quads of this job
-        constexpr int dst = isY ? 256 * c : (isA ? M::ACT0 : P::GOFF) + 256 * c;
-        constexpr int src = isY ? 256 * c : (isA ? M::ACT_IN : 0) + 256 * c;
-        constexpr int rs = isY || isA ? M::XST_W : M::ACT_A4;
+        constexpr int dst = (kind == 0 ? 0 : kind == 1 ? M::F16 : kind == 2 ? M::ACT0 : P::GOFF) + 256 * c;
+        constexpr int src = (kind == 2 ? M::ACT_IN : 0) + 256 * c;
+        constexpr int rs = kind <= 2 ? (kind == 1 ? M::S16 : M::XST_W) : M::ACT_A4;
 #if defined(__HIP_DEVICE_COMPILE__)
         if (lane < nq)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(isY || isA ? xs : gs, (LdsPtr)(buf + row * SRG + dst), 16,
-                                                   16 * lane, ((r0 + row) * rs + src) * 4, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(kind == 0 || kind == 2 ? xs : kind == 1 ? ss : gs,
+                                                   (LdsPtr)(buf + row * SRG + dst), 16, 16 * lane,
+                                                   ((r0 + row) * rs + src) * 4, 0, 0);
 #endif
       }
     });
   };
-  float sv[P::NSV];
-  auto load_static = [&](int h) {               // half-tile h's y0 rows: static features only
-    const int n0 = (h >> 1) * TT + (h & 1) * HT;
-#pragma unroll
-    for (int u = 0; u < P::NSV; ++u) {
-      const int i = tid + u * P::NT;
-      const int tr = i / P::RL, rem = i - tr * P::RL;
-      const int c = rem % M::L;
-      sv[u] = (i < HT * P::RL && c >= 3 && n0 + tr < A.n_traj) ? A.y0[(size_t)(n0 + tr) * P::RL + rem] : 0.f;
-    }
-  };
-  auto put_static = [&](int h) {
-    float* buf = lds + (h & 1) * P::BUF;
-#pragma unroll
-    for (int u = 0; u < P::NSV; ++u) {
-      const int i = tid + u * P::NT;
-      const int tr = i / P::RL, rem = i - tr * P::RL;
-      const int r = rem / M::L, c = rem - r * M::L;
-      if (i < HT * P::RL && c >= 3) buf[tr * SRG + M::F16 + r * (M::L - 3) + c - 3] = sv[u];
-    }
-  };
 
-  if (hb < he) {
-    issue(hb);
-    load_static(hb);
-    put_static(hb);
-    wait_dma();
-    lds_sync();
-  }
+  // pipeline: NBUF - 1 half-tiles in flight; the only vector-memory operations of the loop are the
+  // DMAs, so the wait for the next half-tile at an iteration's end leaves the newest one in flight
+  // (vmcnt(ndma)).
+  constexpr int AHEAD = P::NBUF - 1;
+  #pragma unroll 1
+  for (int h = hb; h < hb + AHEAD && h < he; ++h) issue(h);
+  wait_dma();
+  lds_sync();
   #pragma unroll 1
   for (int h = hb; h < he; ++h) {
-    const bool more = h + 1 < he;
-    if (more) {
-      issue(h + 1);
-      load_static(h + 1);
-    }
-    const float* buf = lds + (h & 1) * P::BUF;
+    const bool more = h + AHEAD < he;
+    if (more) issue(h + AHEAD);
+    const float* buf = bufp(h);
     sfor<P::NRT>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
       if constexpr (P::owner(r) == W) {
@@ -205,8 +204,8 @@ __device__ void gst_body(const GstArgs& A, float* lds) {
         });
       }
     });
-    if (more) put_static(h + 1);
-    wait_dma();
+    if (AHEAD > 1 && more) wait_vm<P::ndma(W)>();   // half-tile h + 1 has landed, h + AHEAD may not have
+    else wait_dma();
     lds_sync();
   }
 

@@ -590,6 +590,17 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     }
     load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
     lds_sync();
+    if constexpr (TRAIN && M::GST) {
+      // the tile's static features once ([tile][16][S16] behind the stored rows): the weight-gradient
+      // GEMM's layer-0 input beside each stage's stored input
+      f4* dst = reinterpret_cast<f4*>(A.ckpt + ckpt_final_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16);
+      constexpr int QS = M::S16 / 4;
+      #pragma unroll 1
+      for (int i = tid; i < TT * QS; i += NTHREADS) {
+        const int t = i / QS, q = i - t * QS;
+        dst[i] = *reinterpret_cast<const f4*>(lds + t * SR + M::XSF_OFF + 4 * q);
+      }
+    }
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
     static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
     lds_sync();
@@ -859,20 +870,26 @@ struct RkAdjointEp {
 // the phase are the partner waves' (mlp_backward_dw).
 // GST: the wave's owned rows of every layer-output gradient also go to `gblk` (this tile-stage's
 // [16][ACT_A4] block, record column order) for ude_gst_dw_kernel.
+// GST (no weight-gradient work, registers to spare): the input-gradient fragments come from `fxp`
+// ([WX_Q(W)] quads, phase d at xq_base(W, d)), each phase's loaded while the previous phase runs
+// (the caller issues the first phase's before the flux pass), so no phase waits on the L2 latency.
 template <class M, int W, int SR, bool DX_ONLY = false, class DW, class DS, class G0, class EP0, class WR>
 __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
-                                             Prof* pf, const EP0& ep0, const WR& wr, float* gblk = nullptr) {
+                                             Prof* pf, const EP0& ep0, const WR& wr, float* gblk = nullptr,
+                                             f4* fxp = nullptr) {
   constexpr bool RW = WR::ON;
+  constexpr bool PF = M::GST && !RW;
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
     constexpr int d = M::D - 1 - decltype(ee)::value;
     // input-gradient fragments go out first; the LDS-only dW GEMMs below hide them
     constexpr int NX = M::XQ(W, d);
-    f4 fx[(NX > 0 && !RW) ? NX : 1];
-    if constexpr (!RW) load_x_frags<M, W, d>(rs, lane, fx);
+    f4 fx[(NX > 0 && !RW && !PF) ? NX : 1];
+    if constexpr (!RW && !PF) load_x_frags<M, W, d>(rs, lane, fx);
     auto FX = [&](int i) -> f4 {
       if constexpr (RW) return wr.wx[M::xq_base(W, d) + i];
+      else if constexpr (PF) return fxp[M::xq_base(W, d) + i];
       else return fx[i];
     };
     // BAYES: this evaluation's eps for the wave's dW tiles (C layout) and bias rows
@@ -1105,6 +1122,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         }
       }
     });
+    if constexpr (PF && d > 0) load_x_frags<M, W, d - 1>(rs, lane, fxp + M::xq_base(W, d - 1));
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
@@ -1569,8 +1587,13 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     // CARRY: the next step's output cotangents are loaded at stage 1 of the step (a whole stage
     // ahead of the flux pass of stage 0 that consumes them)
     float gvc[SL][3];
-    // GST: the next stage's checkpointed input is carried in registers (no LDS staging slot)
+    // GST: the next stage's checkpointed input and activation rows are carried in registers (no LDS
+    // staging slot; the rows' HBM latency runs under the stage's four layer phases), and every phase's
+    // input-gradient fragments are prefetched one phase ahead (mlp_backward PF)
     float ckg[M::GST ? SL : 1][3];
+    constexpr bool GST_A = M::GST && M::STORE_ACT_D;
+    f4 actg[GST_A ? act_q_per_thread<M>() : 1];
+    f4 fxp[M::GST ? M::WX_Q(W) : 1];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's
@@ -1604,7 +1627,17 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         if constexpr (M::STORE_ACT_D) {
           if (jj == 0 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvs);
         }
-        if constexpr (M::STORE_ACT_D && !M::SPLIT_BWD_L && UDE_ABL != 8) {
+        if (GST_A && have_next) {
+          constexpr int QR = M::ACT_A4 / 4;
+#pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * QR) {
+              const int t = i / QR, q = i - t * QR;
+              *reinterpret_cast<f4*>(lds + t * SR + M::ACT0 + 4 * q) = actg[GST_A ? u : 0];
+            }
+          }
+        } else if constexpr (M::STORE_ACT_D && !M::SPLIT_BWD_L && UDE_ABL != 8) {
           // this stage's activation rows straight from the forward's store (issued first: the
           // stage-input copy below runs under their latency)
           constexpr int QR = M::ACT_A4 / 4;
@@ -1717,6 +1750,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           rse = make_rsrc(A.pack + ev * M::PACK_TOTAL, M::PACK_TOTAL * 4);
           es = make_rsrc(A.eslab + ev * M::SLAB_TOTAL, M::SLAB_TOTAL * 4);
         }
+        if constexpr (M::GST) load_x_frags<M, W, M::D - 1>(rse, lane, fxp + M::xq_base(W, M::D - 1));
         // the next stage's checkpointed input: small records (one pair slot per thread)
         // fetch it before the recomputed forward, whose phases then hide the HBM latency;
         // wide ones under the flux pass (registers only live across that pass)
@@ -1781,6 +1815,14 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
         if (!M::SPLIT_BWD_L && !EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
+        if (GST_A && have_next) {
+          const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, nstep, njj));
+#pragma unroll
+          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+            const int i = tid + u * NTHREADS;
+            if (i < TT * (M::ACT_A4 / 4)) actg[GST_A ? u : 0] = src[act_src_q<M>(i)];
+          }
+        }
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (!M::SPLIT_BWD && next_out) {
@@ -1826,7 +1868,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         else mlp_backward<M, W, SR, NO_DW>(rse, es, lds, dw, dws, g0t, lane, pf,
                                            RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr,
                                            M::GST ? A.gst + (((size_t)tile * A.n_steps + step) * 4 + jj) * TT * M::ACT_A4
-                                                  : nullptr);
+                                                  : nullptr, fxp);
         if constexpr (M::SPLITX0) {
           // sum the waves' partial layer-0 input gradients -> RK adjoint (MLP part).  The RK rows
           // use the step-end thread <-> (t, quad) mapping, so the step end needs no barrier.

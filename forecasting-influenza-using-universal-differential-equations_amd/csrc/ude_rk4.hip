@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include "ude_rk4.h"
 #include "ude_entry.h"
+#include "ude_vec.h"      // model-independent vector kernels (compiled in both passes)
 
 // This translation unit is host code only (no kernels are instantiated here).
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -152,6 +153,25 @@ int ude_rhs_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, c
   if (!e) return UDE_E_UNSUPPORTED;
   if (!p) return UDE_E_INVALID;
   return e->rhs_vjp(p, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, (hipStream_t)stream);
+}
+
+int ude_rhs_eval_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x,
+                     const float* cot_f, float* f_out, float f_scale, float* dx, void* ws, float* dparams,
+                     ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p) return UDE_E_INVALID;
+  return e->rhs_eval_vjp(p, pack, x, cot_f, f_out, f_scale, dx, ws, dparams, (hipStream_t)stream);
+}
+
+int ude_lincomb(int64_t n, const float* base, const float* const* k, int32_t nk, const float* coef, float* out,
+                ude_stream_t stream) {
+  return ude::lincomb(n, base, k, nk, coef, out, (hipStream_t)stream);
+}
+
+int ude_scaled_sumsq(int64_t n, const float* err, const float* y0, const float* y1, double atol, double rtol,
+                     double* out, ude_stream_t stream) {
+  return ude::scaled_sumsq(n, err, y0, y1, atol, rtol, out, (hipStream_t)stream);
 }
 
 int ude_pack_decoder(const UdeModelDesc* m, const float* W_dec, const float* b_dec, float* dec_pack,

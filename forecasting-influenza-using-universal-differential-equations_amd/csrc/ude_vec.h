@@ -1,0 +1,97 @@
+// Dense vector kernels of the adaptive step controllers (no model): the stage / solution / error
+// combinations of torchdiffeq's Dormand-Prince step (``y + sum_j beta_j k_j``, a `stack(k) @ c`
+// GEMV in torchdiffeq, a chain of multiply-adds in ude_amd/adaptive.py) as ONE pass over the state,
+// and the error-ratio numerator sum((err / (atol + rtol max(|y0|, |y1|)))^2).  odeint_adjoint's
+// augmented state (y, a_y: 2 N R L floats, plus the parameter adjoint) makes these passes the
+// bulk of an augmented step's memory traffic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ude {
+
+constexpr int LC_MAXK = 8;
+struct LcArgs {
+  const float* base;            // nullable: 0
+  const float* k[LC_MAXK];
+  const float* coef;            // device, nk floats
+  float* out;
+  int64_t n;
+  int nk;
+};
+
+// out = base + sum_j coef[j] k_j; every term accumulated in the fixed order j = 0.. (k_0 first),
+// as the multiply-add chain it replaces: acc = k_0 c_0; acc = fma-free acc + k_j c_j; out = base + acc.
+__global__ __launch_bounds__(256) void ude_lincomb_kernel(LcArgs a) {
+  float c[LC_MAXK];
+#pragma unroll
+  for (int j = 0; j < LC_MAXK; ++j) c[j] = j < a.nk ? a.coef[j] : 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
+    float acc = a.k[0][i] * c[0];
+#pragma unroll
+    for (int j = 1; j < LC_MAXK; ++j)
+      if (j < a.nk) acc = acc + a.k[j][i] * c[j];
+    a.out[i] = a.base ? a.base[i] + acc : acc;
+  }
+}
+
+// Per-block partial sums (fp64) of ((err / tol)^2), tol = atol + rtol * max(|y0|, |y1|) in fp32 as
+// torchdiffeq forms it; out[1 + block] = partial, then ude_sumsq_finish sums them in order into out[0].
+constexpr int SSQ_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void ude_scaled_sumsq_kernel(const float* __restrict__ err,
+                                                               const float* __restrict__ y0,
+                                                               const float* __restrict__ y1, float atol,
+                                                               float rtol, int64_t n, double* __restrict__ out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float tol = atol + rtol * fmaxf(fabsf(y0[i]), fabsf(y1[i]));
+    const float r = err[i] / tol;
+    s += (double)r * (double)r;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(64) void ude_sumsq_finish_kernel(double* __restrict__ out, int nb) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 64) s += out[1 + i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+inline int lincomb(int64_t n, const float* base, const float* const* k, int nk, const float* coef, float* out,
+                   hipStream_t s) {
+  if (n < 0 || nk < 1 || nk > LC_MAXK || !k || !coef || !out) return -2;
+  if (n == 0) return 0;
+  LcArgs a;
+  a.base = base;
+  for (int j = 0; j < LC_MAXK; ++j) a.k[j] = j < nk ? k[j] : nullptr;
+  for (int j = 0; j < nk; ++j)
+    if (!k[j]) return -2;
+  a.coef = coef; a.out = out; a.n = n; a.nk = nk;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(ude_lincomb_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+inline int scaled_sumsq(int64_t n, const float* err, const float* y0, const float* y1, double atol, double rtol,
+                        double* out, hipStream_t s) {
+  if (n < 0 || !err || !y0 || !y1 || !out) return -2;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > SSQ_BLOCKS) blocks = SSQ_BLOCKS;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(ude_scaled_sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, s, err, y0, y1, (float)atol,
+                     (float)rtol, n, out);
+  hipLaunchKernelGGL(ude_sumsq_finish_kernel, dim3(1), dim3(64), 0, s, out, (int)blocks);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace ude

@@ -41,7 +41,8 @@ EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_
                     "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_rhs_workspace",
                     "ude_rhs_forward", "ude_rhs_vjp", "ude_pack_decoder", "ude_rk4_forward_dec",
                     "ude_decoder_backward", "ude_nll_workspace", "ude_nll_forward", "ude_nll_backward",
-                    "ude_build_info")
+                    "ude_rhs_eval_vjp", "ude_lincomb", "ude_scaled_sumsq", "ude_build_info")
+SUMSQ_WS = 1025          # doubles of ude_scaled_sumsq's output / workspace (UDE_SUMSQ_WS)
 
 
 class UdeModelDesc(ctypes.Structure):
@@ -151,6 +152,12 @@ class NativeLib:
         L.ude_nll_forward.restype = i32
         L.ude_nll_backward.argtypes = [pdesc, i32, i32, i32, vp, vp, vp, vp, vp, vp]
         L.ude_nll_backward.restype = i32
+        L.ude_rhs_eval_vjp.argtypes = [pdesc, pprob, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp]
+        L.ude_rhs_eval_vjp.restype = i32
+        L.ude_lincomb.argtypes = [ctypes.c_int64, vp, pvp, ctypes.c_int32, vp, vp, vp]
+        L.ude_lincomb.restype = i32
+        L.ude_scaled_sumsq.argtypes = [ctypes.c_int64, vp, vp, vp, dbl, dbl, vp, vp]
+        L.ude_scaled_sumsq.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
 
@@ -241,6 +248,18 @@ class NativeLib:
     def rhs_vjp(self, desc, prob, pack, x, cot_f, cot_rates, cot_fa, dx, ws, dparams, stream) -> None:
         check(self.lib.ude_rhs_vjp(ctypes.byref(desc), ctypes.byref(prob), pack, x, cot_f, cot_rates, cot_fa, dx,
                                    ws, dparams, stream), "ude_rhs_vjp")
+
+    def rhs_eval_vjp(self, desc, prob, pack, x, cot_f, f_out, f_scale, dx, ws, dparams, stream) -> None:
+        check(self.lib.ude_rhs_eval_vjp(ctypes.byref(desc), ctypes.byref(prob), pack, x, cot_f, f_out,
+                                        float(f_scale), dx, ws, dparams, stream), "ude_rhs_eval_vjp")
+
+    def lincomb(self, n, base, ks: Sequence[int], coef, out, stream) -> None:
+        arr = (ctypes.c_void_p * len(ks))(*ks)
+        check(self.lib.ude_lincomb(int(n), base, arr, len(ks), coef, out, stream), "ude_lincomb")
+
+    def scaled_sumsq(self, n, err, y0, y1, atol, rtol, out, stream) -> None:
+        check(self.lib.ude_scaled_sumsq(int(n), err, y0, y1, float(atol), float(rtol), out, stream),
+              "ude_scaled_sumsq")
 
     def pack_decoder(self, desc, W, b, out, stream) -> None:
         check(self.lib.ude_pack_decoder(ctypes.byref(desc), W, b, out, stream), "ude_pack_decoder")

@@ -94,10 +94,15 @@ def _dot(ks: List[torch.Tensor], c: torch.Tensor) -> torch.Tensor:
 
 
 def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,
-                 max_num_steps: int = MAX_NUM_STEPS, norm=None) -> torch.Tensor:
+                 max_num_steps: int = MAX_NUM_STEPS, norm=None, vec=None) -> torch.Tensor:
     """``norm``: torchdiffeq's error norm (default the RMS over every element, ``_rms_norm``);
-    odeint_adjoint passes its mixed norm over the augmented state's pieces."""
+    odeint_adjoint passes its mixed norm over the augmented state's pieces.  ``vec`` (optional):
+    ``vec.comb(base, ks, c)`` = base + sum_j c[j] ks[j] and ``vec.ratio(err, y, y1)`` = the error
+    ratio, each one pass over the state (odeint_adjoint's fused path: ude_lincomb /
+    ude_scaled_sumsq) instead of a chain of PyTorch operators.  The dense-output coefficients are
+    formed only for the step an output time falls in (same arithmetic, not per accepted step)."""
     _rms = _rms_default if norm is None else norm
+    comb = (lambda base, ks, c: (_dot(ks, c) if base is None else base + _dot(ks, c))) if vec is None else vec.comb
     ydt = y0.dtype
     dev = y0.device
     tt = t.to(device=dev, dtype=torch.float64)
@@ -129,7 +134,7 @@ def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
     y, fy = y0, f0
     t_end = t0
     seg_t0 = t0
-    coef = None
+    last = None        # the last accepted step: (y, f(y), y1, f(y1), ks, dt)
     n_steps = 0
     for i in range(1, len(tt)):
         next_t = tt[i]
@@ -145,27 +150,33 @@ def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
             ks = [fy]
             yi = y
             for s in range(6):
-                yi = y + _dot(ks, beta[s] * dts)
+                yi = comb(y, ks, beta[s] * dts)
                 ti = te if _ALPHA[s] == 1.0 else ts + _ALPHA[s] * dt
                 ks.append(func(ti.to(ydt), yi))
             y1, f1 = yi, ks[-1]
-            err = _dot(ks, dts * c_err)
-            ratio = _rms(err / (at + rt * torch.max(y.abs(), y1.abs()))).abs()
+            err = comb(None, ks, dts * c_err)
+            if vec is None:
+                ratio = _rms(err / (at + rt * torch.max(y.abs(), y1.abs()))).abs()
+            else:
+                ratio = vec.ratio(err, y, y1)
             n_steps += 1
-            if bool(ratio <= 1):
-                y_mid = y + _dot(ks, dts * c_mid)
-                a = 2 * dts * (f1 - fy) - 8 * (y1 + y) + 16 * y_mid
-                b = dts * (5 * fy - 3 * f1) + 18 * y + 14 * y1 - 32 * y_mid
-                c = dts * (f1 - 4 * fy) - 11 * y - 5 * y1 + 16 * y_mid
-                coef = [y, dts * fy, c, b, a]
+            rf = float(ratio)                        # one host read per attempt
+            if rf <= 1:
+                last = (y, fy, y1, f1, ks, dts)
                 seg_t0, t_end = ts, te
                 y, fy = y1, f1
-            if ratio == 0:
+            if rf == 0:
                 dt = dt * 10.0
             else:
-                dfac = 1.0 if ratio < 1 else 0.2
+                dfac = 1.0 if rf < 1 else 0.2
                 fac = torch.clamp(0.9 / ratio.to(torch.float64) ** 0.2, min=dfac, max=10.0)
                 dt = dt * fac
+        yl, fyl, y1l, f1l, ksl, dtl = last
+        y_mid = comb(yl, ksl, dtl * c_mid)
+        a = 2 * dtl * (f1l - fyl) - 8 * (y1l + yl) + 16 * y_mid
+        b = dtl * (5 * fyl - 3 * f1l) + 18 * yl + 14 * y1l - 32 * y_mid
+        c = dtl * (f1l - 4 * fyl) - 11 * yl - 5 * y1l + 16 * y_mid
+        coef = [yl, dtl * fyl, c, b, a]
         x = ((next_t - seg_t0) / (t_end - seg_t0)).to(ydt)
         total = coef[0] + x * coef[1]
         xp = x

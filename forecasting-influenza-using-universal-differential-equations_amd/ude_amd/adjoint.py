@@ -17,10 +17,15 @@ the specification is torchdiffeq's published algorithm:
 * the forward solve runs under no_grad, so quantities the RHS records on the side (params /
   tracker, hence posterior() / the Fa norm) carry no gradient, as in torchdiffeq.
 
-Every augmented evaluation calls the RHS module and ``torch.autograd.grad`` through it: for
-the UDE modules on a HIP device that is one gfx950 evaluation kernel + one VJP kernel
-(ude_amd/eval_rhs.py).  The augmented state lives in one flat tensor (torchdiffeq's
-``_TupleFunc`` flattening) stepped by ude_amd.adaptive.eager_dopri5 or the fixed grids.
+The augmented state lives in one flat tensor (torchdiffeq's ``_TupleFunc`` flattening) stepped by
+ude_amd.adaptive.eager_dopri5 or the fixed grids.  For a deterministic UDE module on a HIP device
+(the adjoint parameters its own, in C-ABI order; t without gradient) the backward is fused
+(``_FusedAug``): the weights are packed once, every reversed augmented evaluation
+``(-vjp_t, -f, a^T df/dy, a^T df/dtheta)`` is ONE gfx950 launch (ude_rhs_eval_vjp: evaluation and
+VJP, written straight into the flat derivative), and the Dormand-Prince stage / error / dense-output
+combinations are single passes (ude_lincomb, ude_scaled_sumsq).  Otherwise every augmented
+evaluation calls the RHS module and ``torch.autograd.grad`` through it (for the UDE modules on a
+HIP device one evaluation kernel + one VJP kernel, ude_amd/eval_rhs.py).
 """
 from __future__ import annotations
 
@@ -63,8 +68,85 @@ def find_parameters(module) -> List[torch.Tensor]:
     return [p for p in module.parameters() if p.requires_grad]
 
 
+SUMSQ_WS = 1025          # doubles per ude_scaled_sumsq output (UDE_SUMSQ_WS)
+
+
+class _FusedAug:
+    """The reversed augmented dynamics of a deterministic UDE module on a HIP device, fused.
+
+    Flat state [vjp_t | y (N, R, L) | a_y (N, R, L) | a_theta (params, C-ABI order)]; its derivative
+    in s = -t is [-vjp_t', -f(y), a_y^T df/dy, a_y^T df/dtheta] = ude_rhs_eval_vjp with cot = a_y and
+    f scaled by -1, written into the output vector's slices by one launch (+ the deterministic
+    gradient reductions).  ``comb`` / ``ratio`` are the controller's dense passes (eager_dopri5's
+    ``vec``): ude_lincomb, and the mixed error norm with the y / a_y pieces' sums of squares from
+    ude_scaled_sumsq (the parameter pieces are small and stay PyTorch)."""
+
+    def __init__(self, func, y: torch.Tensor, adjoint_params, seminorm: bool):
+        from . import eval_rhs
+        from . import fused as _fused
+        self.plan = eval_rhs._plan(eval_rhs.deterministic_config(func), y.shape[0], func.fa_weight(), y.device)
+        self.lib = self.plan.lib
+        self.stream = _fused._stream(y.device)
+        lins = func.ude_linears()
+        ws_ = [l.weight.detach().contiguous() for l in lins]
+        bs_ = [l.bias.detach().contiguous() for l in lins]
+        self.pack = torch.empty(self.plan.sizes.pack_bytes // 4, dtype=torch.float32, device=y.device)
+        self.lib.pack(self.plan.desc, [w.data_ptr() for w in ws_], [b.data_ptr() for b in bs_], self.pack.data_ptr(),
+                      self.stream)
+        self.ws = torch.empty(max(self.plan.ws_bytes // 4, 1), dtype=torch.float32, device=y.device)
+        self.nrl = int(y.numel())
+        self.psizes = [int(p.numel()) for p in adjoint_params]
+        self.seminorm = seminorm
+        self.ssq = torch.empty(2 * SUMSQ_WS, dtype=torch.float64, device=y.device)
+        self.evals = 0
+
+    @staticmethod
+    def eligible(func, y: torch.Tensor, adjoint_params, t_requires_grad: bool) -> bool:
+        from . import eval_rhs
+        from .rhs import _UDEModule
+        if t_requires_grad or not isinstance(func, _UDEModule) or func.uncertainty != "none":
+            return False
+        if not (y.is_cuda and y.dtype == torch.float32 and y.dim() == 3 and eval_rhs.eligible(func, y)):
+            return False
+        abi = []
+        for lin in func.ude_linears():
+            abi += [lin.weight, lin.bias]
+        return [id(p) for p in adjoint_params] == [id(p) for p in abi]
+
+    def __call__(self, s, yf: torch.Tensor) -> torch.Tensor:
+        self.evals += 1
+        out = torch.empty_like(yf)
+        out[:1].zero_()
+        b, ob, n = yf.data_ptr(), out.data_ptr(), self.nrl
+        self.lib.rhs_eval_vjp(self.plan.desc, self.plan.prob, self.pack.data_ptr(), b + 4, b + 4 * (1 + n), ob + 4,
+                              -1.0, ob + 4 * (1 + n), self.ws.data_ptr(), ob + 4 * (1 + 2 * n), self.stream)
+        return out
+
+    def comb(self, base, ks, c) -> torch.Tensor:
+        out = torch.empty_like(ks[0])
+        c = c.to(torch.float32).contiguous()
+        self.lib.lincomb(out.numel(), None if base is None else base.data_ptr(), [k.data_ptr() for k in ks],
+                         c.data_ptr(), out.data_ptr(), self.stream)
+        self._keep = c                                    # alive until the stream has read it
+        return out
+
+    def ratio(self, err, y, y1, atol: float, rtol: float) -> torch.Tensor:
+        n = self.nrl
+        for i, off in enumerate((1, 1 + n)):
+            self.lib.scaled_sumsq(n, err.data_ptr() + 4 * off, y.data_ptr() + 4 * off, y1.data_ptr() + 4 * off,
+                                  atol, rtol, self.ssq.data_ptr() + 8 * i * SUMSQ_WS, self.stream)
+        tol0 = atol + rtol * torch.max(y[:1].abs(), y1[:1].abs())
+        parts = [(err[:1] / tol0).abs().reshape(()).double(),
+                 (self.ssq[0] / n).sqrt(), (self.ssq[SUMSQ_WS] / n).sqrt()]
+        if not self.seminorm and self.psizes:
+            off = 1 + 2 * n
+            r = err[off:] / (atol + rtol * torch.max(y[off:].abs(), y1[off:].abs()))
+            parts += [_rms(x).double() for x in torch.split(r, self.psizes)]
+        return torch.max(torch.stack(parts))
+
+
 def _solve_segment(aug_func, flat: _Flat, state: List[torch.Tensor], t_from, t_to, rtol, atol, method, options,
-                   norm_of_tuple):
+                   norm_of_tuple, fused: "_FusedAug" = None):
     """odeint(augmented_dynamics, state, [t_from, t_to]) with t_to < t_from, returning the state
     at t_to: solved forwards in s = -t on the negated function (torchdiffeq _ReverseFunc)."""
     y0 = flat.flat(state)
@@ -80,11 +162,18 @@ def _solve_segment(aug_func, flat: _Flat, state: List[torch.Tensor], t_from, t_t
     opts = dict(options or {})
     if method == "dopri5":
         norm = lambda v: norm_of_tuple(flat.split(v))
-        sol = _adaptive.eager_dopri5(f_rev, y0, s_pair, rtol, atol, opts.pop("first_step", None),
-                                     opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS), norm=norm)
+        vec = None
+        if fused is not None:
+            class _Vec:
+                comb = staticmethod(fused.comb)
+                ratio = staticmethod(lambda err, y, y1: fused.ratio(err, y, y1, float(atol), float(rtol)))
+            vec = _Vec
+        sol = _adaptive.eager_dopri5(f_rev if fused is None else fused, y0, s_pair, rtol, atol,
+                                     opts.pop("first_step", None), opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS),
+                                     norm=norm, vec=vec)
     elif method in ("rk4", "euler", "midpoint"):
         from .solvers import eager_fixed_grid
-        sol = eager_fixed_grid(f_rev, y0, s_pair, method, opts.pop("step_size", None))
+        sol = eager_fixed_grid(f_rev if fused is None else fused, y0, s_pair, method, opts.pop("step_size", None))
     else:
         raise NotImplementedError(f"adjoint_method '{method}' is not implemented (dopri5 / rk4 / euler / midpoint are)")
     return flat.split(sol[1])
@@ -125,6 +214,8 @@ class _OdeintAdjoint(torch.autograd.Function):
         lens = [len(x) for x in lists]
 
         counts = {"evals": 0}
+        fused = _FusedAug(func, y[-1], adjoint_params, seminorm) \
+            if _FusedAug.eligible(func, y[-1], adjoint_params, t_requires_grad) else None
 
         def augmented_dynamics(tt, y_aug):
             counts["evals"] += 1
@@ -156,7 +247,7 @@ class _OdeintAdjoint(torch.autograd.Function):
                     aug_state[0] = aug_state[0] - dLd_cur_t
                     time_vjps[i] = dLd_cur_t
                 aug_state = list(_solve_segment(augmented_dynamics, flat, aug_state, t[i], t[i - 1], adjoint_rtol,
-                                                adjoint_atol, adjoint_method, options, adjoint_norm))
+                                                adjoint_atol, adjoint_method, options, adjoint_norm, fused))
                 aug_state[1] = y[i - 1]
                 aug_state[2] = aug_state[2] + grad_y[i - 1]
             if t_requires_grad:
@@ -164,7 +255,8 @@ class _OdeintAdjoint(torch.autograd.Function):
                 # vjp_t dynamics (torchdiffeq: time_vjps[0] = aug_state[0], no negation)
                 time_vjps[0] = aug_state[0]
         try:
-            func.last_adjoint_info = {"augmented_evals": counts["evals"], "seminorm": seminorm}
+            func.last_adjoint_info = {"augmented_evals": counts["evals"] + (fused.evals if fused else 0),
+                                      "seminorm": seminorm, "fused": fused is not None}
         except AttributeError:
             pass
         adj_y = aug_state[2]

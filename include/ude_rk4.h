@@ -271,6 +271,27 @@ int ude_nll_forward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, cons
 int ude_nll_backward(const UdeModelDesc* m, int32_t T, int32_t S, int32_t B, const float* yhat, const float* y,
                      const float* grad, const void* ws, float* dyhat, ude_stream_t stream);
 
+/* ---- odeint_adjoint's augmented dynamics (torchdiffeq adjoint; the solver API lib/VAE.py:5 imports) --
+ * One evaluation of the right-hand side and its VJP in ONE launch: f_out = f_scale * f(x) (N, R, L),
+ * dx = cot_f^T df/dx (N, R, L) and dparams = cot_f^T df/dtheta (torch parameter order).  The reversed
+ * augmented dynamics of odeint_adjoint's backward, (-f, a^T df/dy, a^T df/dtheta), are f_scale = -1,
+ * cot_f = a; replaces the module call + torch.autograd.grad per augmented evaluation.  Deterministic
+ * kinds; ws: ude_rhs_workspace() bytes. */
+int ude_rhs_eval_vjp(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const float* x,
+                     const float* cot_f, float* f_out, float f_scale, float* dx, void* ws, float* dparams,
+                     ude_stream_t stream);
+
+/* Dense passes of the adaptive step controllers (torchdiffeq's Dormand-Prince step; no model).
+ * ude_lincomb: out[i] = base[i] + sum_j coef[j] * k[j][i] over n floats (base nullable: 0; coef a
+ * DEVICE array of nk <= 8 floats; k a host array of nk device pointers), one pass.
+ * ude_scaled_sumsq: out[0] (device fp64) = sum_i (err_i / (atol + rtol * max(|y0_i|, |y1_i|)))^2
+ * (the error ratio's numerator, tolerance formed in fp32); out must hold UDE_SUMSQ_WS doubles. */
+#define UDE_SUMSQ_WS 1025
+int ude_lincomb(int64_t n, const float* base, const float* const* k, int32_t nk, const float* coef, float* out,
+                ude_stream_t stream);
+int ude_scaled_sumsq(int64_t n, const float* err, const float* y0, const float* y1, double atol, double rtol,
+                     double* out, ude_stream_t stream);
+
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);
 

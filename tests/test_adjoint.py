@@ -161,8 +161,60 @@ def test_fused_adjoint_matches_oracle(pkg, kind, R):
     yg = y0.to("cuda").requires_grad_(True)
     ys = odeint_adjoint(mg, yg, t.to("cuda"), rtol=rtol, atol=atol)
     (ys * c.to("cuda")).sum().backward()
+    assert mg.last_adjoint_info["fused"], mg.last_adjoint_info     # one eval+VJP launch per evaluation
     assert normwise_rel(ys.detach(), yr) < 1e-5
     assert normwise_rel(yg.grad, dy0) < bar(d32, dy0), normwise_rel(yg.grad, dy0)
     grads = [p.grad for lin in mg.ude_linears() for p in (lin.weight, lin.bias)]
     for i, (a, b) in enumerate(zip(grads, dps)):
         assert normwise_rel(a, b) < bar(p32[i], b), (i, normwise_rel(a, b), bar(p32[i], b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm", [None, "seminorm"])
+def test_fused_adjoint_matches_autograd_adjoint(pkg, norm):
+    """The fused backward (ude_rhs_eval_vjp per augmented evaluation, ude_lincomb / ude_scaled_sumsq
+    controller passes) against the generic one (module call + torch.autograd.grad per evaluation,
+    PyTorch controller), selected by handing the parameters in another order: same gradients."""
+    from torchdiffeq import odeint_adjoint
+    torch.manual_seed(4)
+    mod = pkg.FaFp(49, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]).to("cuda")
+    y0 = _y0(300, 49, torch.float32).to("cuda")
+    t = torch.tensor([0.0, 0.7, 1.5], device="cuda")
+    c = torch.randn((3,) + tuple(y0.shape), generator=torch.Generator().manual_seed(5)).to("cuda")
+    opts = None if norm is None else dict(norm=norm)
+    params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
+    out = []
+    for order in (params, params[::-1]):
+        mod.zero_grad(set_to_none=True)
+        yg = y0.clone().requires_grad_(True)
+        ys = odeint_adjoint(mod, yg, t, rtol=1e-6, atol=1e-8, adjoint_params=order, adjoint_options=opts)
+        (ys * c).sum().backward()
+        out.append((mod.last_adjoint_info["fused"], yg.grad.clone(), [p.grad.clone() for p in params]))
+    assert out[0][0] and not out[1][0]
+    assert normwise_rel(out[0][1], out[1][1]) < 1e-5
+    for a, b in zip(out[0][2], out[1][2]):
+        assert normwise_rel(a, b) < 1e-5
+
+
+@pytest.mark.gpu
+def test_controller_vector_passes_match_torch(pkg):
+    """ude_lincomb (out = base + sum_j c_j k_j, one pass) and ude_scaled_sumsq (sum of squared error
+    ratios, fp32 tolerance, fp64 sums) against PyTorch on a ragged length."""
+    from ude_amd import _native, fused
+    lib = _native.prebuilt()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    n = 1_000_003
+    ks = [torch.randn(n, device="cuda", generator=g) for _ in range(7)]
+    base = torch.randn(n, device="cuda", generator=g)
+    c = torch.randn(7, device="cuda", generator=g)
+    out = torch.empty(n, device="cuda")
+    st = fused._stream(torch.device("cuda"))
+    for nk in (1, 4, 7):
+        lib.lincomb(n, base.data_ptr(), [k.data_ptr() for k in ks[:nk]], c.data_ptr(), out.data_ptr(), st)
+        ref = base + sum(ks[j] * c[j] for j in range(nk))
+        assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
+    ssq = torch.empty(_native.SUMSQ_WS, dtype=torch.float64, device="cuda")
+    y0, y1 = ks[1], ks[2]
+    lib.scaled_sumsq(n, ks[0].data_ptr(), y0.data_ptr(), y1.data_ptr(), 1e-8, 1e-6, ssq.data_ptr(), st)
+    r = (ks[0] / (1e-8 + 1e-6 * torch.max(y0.abs(), y1.abs()))).double()
+    assert abs(float(ssq[0]) / float((r * r).sum()) - 1) < 1e-6

@@ -29,7 +29,8 @@ NPROF = 20
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "state49"      # [--build]: compile only (on the host)
     w = bench.WORKLOADS[wl]
-    cfg = (w["kind"], w["R"], w["L"], tuple(w["net"]) if w["net"] else None, tuple(w["aug"]) if w["aug"] else None)
+    kind = "B" + w["kind"][len("Bayes_"):] if w["kind"].startswith("Bayes_") else w["kind"]
+    cfg = (kind, w["R"], w["L"], tuple(w["net"]) if w["net"] else None, tuple(w["aug"]) if w["aug"] else None)
     path = os.path.join(_native.BUILD, f"libude_rk4_profile_{wl}.so")
     if "--build" in sys.argv or not os.path.exists(path):
         _native.build_library([cfg], path, "profile_" + wl, jobs=1, extra_flags=["-DUDE_PROFILE"])

@@ -878,7 +878,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
                                              Prof* pf, const EP0& ep0, const WR& wr, float* gblk = nullptr,
                                              f4* fxp = nullptr) {
   constexpr bool RW = WR::ON;
-  constexpr bool PF = M::GST && !RW;
+  constexpr bool PF = M::PF_X && !RW;
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
@@ -1593,7 +1593,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     float ckg[M::GST ? SL : 1][3];
     constexpr bool GST_A = M::GST && M::STORE_ACT_D;
     f4 actg[GST_A ? act_q_per_thread<M>() : 1];
-    f4 fxp[M::GST ? M::WX_Q(W) : 1];
+    f4 fxp[M::PF_X ? M::WX_Q(W) : 1];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's
@@ -1750,7 +1750,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           rse = make_rsrc(A.pack + ev * M::PACK_TOTAL, M::PACK_TOTAL * 4);
           es = make_rsrc(A.eslab + ev * M::SLAB_TOTAL, M::SLAB_TOTAL * 4);
         }
-        if constexpr (M::GST) load_x_frags<M, W, M::D - 1>(rse, lane, fxp + M::xq_base(W, M::D - 1));
+        if constexpr (M::PF_X) load_x_frags<M, W, M::D - 1>(rse, lane, fxp + M::xq_base(W, M::D - 1));
         // the next stage's checkpointed input: small records (one pair slot per thread)
         // fetch it before the recomputed forward, whose phases then hide the HBM latency;
         // wide ones under the flux pass (registers only live across that pass)

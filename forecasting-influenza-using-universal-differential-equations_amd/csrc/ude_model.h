@@ -215,6 +215,10 @@ struct Model {
   static constexpr bool SPLIT_BWD_L = false;
 #endif
   static constexpr bool SPLITB = SPLIT_BWD || SPLIT_BWD_L;
+  // Backward critical path without weight-gradient accumulators (GST; SPLIT_BWD_L's waves 0-3) and
+  // weights read from L2 (never register-resident at these sizes): each phase's input-gradient fragments are loaded one phase
+  // ahead (the first phase's before the flux pass), so no phase waits on the L2 latency
+  static constexpr bool PF_X = GST || SPLIT_BWD_L;
   static constexpr int BWD_THREADS = SPLITB ? 2 * NTHREADS : NTHREADS;
   // Training forward of small records at one tile per CU: four more waves copy each stage's
   // activation rows from the record to HBM during the flux pass, off the critical path

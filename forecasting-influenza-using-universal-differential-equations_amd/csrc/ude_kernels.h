@@ -873,12 +873,13 @@ struct RkAdjointEp {
 // GST (no weight-gradient work, registers to spare): the input-gradient fragments come from `fxp`
 // ([WX_Q(W)] quads, phase d at xq_base(W, d)), each phase's loaded while the previous phase runs
 // (the caller issues the first phase's before the flux pass), so no phase waits on the L2 latency.
-template <class M, int W, int SR, bool DX_ONLY = false, class DW, class DS, class G0, class EP0, class WR>
+template <class M, int W, int SR, bool DX_ONLY = false, bool PFX = false, class DW, class DS, class G0, class EP0,
+          class WR>
 __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& dw, DS& dws, G0& g0t, int lane,
                                              Prof* pf, const EP0& ep0, const WR& wr, float* gblk = nullptr,
                                              f4* fxp = nullptr) {
   constexpr bool RW = WR::ON;
-  constexpr bool PF = M::PF_X && !RW;
+  constexpr bool PF = PFX && !RW;     // only the RK4 backward (bwd_body) hands over the fxp array
   const int t = lane & 15, g = lane >> 4;
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
@@ -1865,7 +1866,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         lds_sync();
         UDE_STAMP(pf, 11);
         if constexpr (UDE_ABL == 7) sfor<M::D>([&](auto) { lds_sync(); });
-        else mlp_backward<M, W, SR, NO_DW>(rse, es, lds, dw, dws, g0t, lane, pf,
+        else mlp_backward<M, W, SR, NO_DW, M::PF_X>(rse, es, lds, dw, dws, g0t, lane, pf,
                                            RkAdjointEp<M, SR>{lds + t16 * SR, dt, jj}, wr,
                                            M::GST ? A.gst + (((size_t)tile * A.n_steps + step) * 4 + jj) * TT * M::ACT_A4
                                                   : nullptr, fxp);

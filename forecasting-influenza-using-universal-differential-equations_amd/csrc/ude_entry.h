@@ -103,6 +103,22 @@ struct Ops {
   }
   static int64_t gst_rows_floats(int n_tiles, int n_steps) { return (int64_t)n_tiles * n_steps * 4 * TT * M::ACT_A4; }
 
+  // FULL0: the output cotangents of the static latent dims, summed over the output times into dy0
+  static hipError_t static_tsum(const UdeProblem* p, const float* dlatent, float* dy0, hipStream_t s) {
+    if constexpr (M::FULL0) {
+      if (dlatent) {
+        const long total = (long)p->n_traj * M::R * (M::L - 3);
+        long blocks = (total + 255) / 256;
+        if (blocks > 4096) blocks = 4096;
+        if (blocks < 1) blocks = 1;
+        hipLaunchKernelGGL((ude_static_tsum_kernel<M>), dim3((unsigned)blocks), dim3(256), 0, s, dlatent, p->n_traj,
+                           p->n_out + 1, dy0);
+        return hipGetLastError();
+      }
+    }
+    return hipSuccess;
+  }
+
   // UdeProblem.recompute: the Recompute<M> view of the model (no stored activations; GST needs them)
   static constexpr bool RC_VIEW = M::ACT_STORED && !M::GST;
   static bool rc(const UdeProblem* p) { return RC_VIEW && p->recompute; }
@@ -398,6 +414,7 @@ struct Ops {
       float* part = slab + gst_rows_floats(n_tiles, p->n_steps);
       hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
       HIPCHK(hipGetLastError());
+      HIPCHK(static_tsum(p, dlatent, dy0, s));
       if (ne > 0) {
         GstArgs ga;
         ga.ckpt = ckpt; ga.gst = slab; ga.y0 = y0; ga.part = part;
@@ -412,6 +429,7 @@ struct Ops {
     }
     hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
+    HIPCHK(static_tsum(p, dlatent, dy0, s));
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());

@@ -1594,6 +1594,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     float ckg[M::GST ? SL : 1][3];
     constexpr bool GST_A = M::GST && M::STORE_ACT_D;
     f4 actg[GST_A ? act_q_per_thread<M>() : 1];
+    float gvg[GST_A ? SL : 1][3];          // GST: the next step's output cotangents, loaded a stage ahead
     f4 fxp[M::PF_X ? M::WX_Q(W) : 1];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
@@ -1625,7 +1626,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // large records: the step's output cotangents are loaded at its last stage's start, with
         // the activation rows (their latency is paid there anyway), not right before the flux pass
         float gvs[M::STORE_ACT_D ? SL : 1][3];
-        if constexpr (M::STORE_ACT_D) {
+        if constexpr (M::STORE_ACT_D && !GST_A) {
           if (jj == 0 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvs);
         }
         if (GST_A && have_next) {
@@ -1815,19 +1816,12 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
         // flux backward: d k_j -> d q (pre-|.| rates), d Fa, and the direct d Y.
         // One item = one trajectory x a group of 4 regions (12 features, 8 rates):
         // every record access is a 16-B LDS op.
-        if (!M::SPLIT_BWD_L && !EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
-        if (GST_A && have_next) {
-          const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, nstep, njj));
-#pragma unroll
-          for (int u = 0; u < act_q_per_thread<M>(); ++u) {
-            const int i = tid + u * NTHREADS;
-            if (i < TT * (M::ACT_A4 / 4)) actg[GST_A ? u : 0] = src[act_src_q<M>(i)];
-          }
-        }
+        if (!M::SPLIT_BWD_L && !GST_A && !EARLY_CK && have_next) ckpt_issue<M>(A, tile, nstep, njj, ckn);
         if constexpr (!M::ACT_STORED) flux_backward<M, SR>(lds, A, n0, jj, dt, ca, cb, mu, cn);
         UDE_STAMP(pf, 16);
         if (!M::SPLIT_BWD && next_out) {
-          if constexpr (M::STORE_ACT_D) out_finish<M>(A, sc, nstep, n0, gvs, sgn, pgn);
+          if constexpr (GST_A) out_finish<M>(A, sc, nstep, n0, gvg, sgn, pgn);
+          else if constexpr (M::STORE_ACT_D) out_finish<M>(A, sc, nstep, n0, gvs, sgn, pgn);
           else if constexpr (!CARRY) out_finish<M>(A, sc, nstep, n0, gvn, sgn, pgn);
           // step nstep's output cotangents: the y_{n+1} share joins PEND (RK_A of the
           // next step = ACCY + PEND), the y_n share is staged in DK3 (dead at jj == 0)
@@ -1845,7 +1839,20 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
           });
         }
         UDE_STAMP(pf, 17);
-        if (M::GST && !CARRY && have_next) {
+        if constexpr (GST_A) {
+          if (have_next) {
+            // the next stage's input, activation rows and (a stage ahead of their consumer) output
+            // cotangents, issued only after this stage's waits: no wait until the next stage start
+            ckpt_issue<M>(A, tile, nstep, njj, ckg);
+            const f4* src = reinterpret_cast<const f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, nstep, njj));
+#pragma unroll
+            for (int u = 0; u < act_q_per_thread<M>(); ++u) {
+              const int i = tid + u * NTHREADS;
+              if (i < TT * (M::ACT_A4 / 4)) actg[u] = src[act_src_q<M>(i)];
+            }
+            if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvg);
+          }
+        } else if (M::GST && !CARRY && have_next) {
 #pragma unroll
           for (int sl = 0; sl < (M::GST ? SL : 1); ++sl)
 #pragma unroll
@@ -1928,22 +1935,16 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
       }
     }
     if constexpr (M::FULL0) {
-      // static latent dims: the summed input gradient of every evaluation plus the
-      // direct cotangent of every output time (they are carried unchanged)
-      const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+      // static latent dims: the summed input gradient of every evaluation (the direct cotangent of
+      // every output time -- they are carried unchanged -- is added by ude_static_tsum_kernel, a
+      // coalesced pass over d latent outside this latency-bound loop)
       #pragma unroll 1
       for (int i = tid; i < TT * M::S; i += NTHREADS) {
         const int t = i / M::S, s = i - t * M::S;
         const int n = n0 + t;
         if (n < A.n_traj) {
           const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
-          const size_t base = ((size_t)n * M::R + r) * M::L + c;
-          float v = lds[t * SR + M::DYS_OFF + s];
-          if (A.dlatent) {
-            #pragma unroll 4
-            for (int jt = 0; jt <= A.n_out; ++jt) v += A.dlatent[(size_t)jt * NRL + base];
-          }
-          A.dy0[base] = v;
+          A.dy0[((size_t)n * M::R + r) * M::L + c] = lds[t * SR + M::DYS_OFF + s];
         }
       }
     }
@@ -1968,6 +1969,23 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
 #endif
 }
+// FULL0 (Bayesian RHS, static dims in the solve's layer 0): dy0[n, r, c >= 3] += sum_j dlatent[j, n, r, c]
+// in output order j (the same additions as one loop after the input-gradient sum).
+template <class M>
+__global__ __launch_bounds__(256) void ude_static_tsum_kernel(const float* __restrict__ dlatent, int n_traj,
+                                                              int n_times, float* __restrict__ dy0) {
+  constexpr int SPR = M::L - 3;
+  const size_t NRL = (size_t)n_traj * M::R * M::L, total = (size_t)n_traj * M::R * SPR;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const size_t nr = i / SPR;
+    const size_t base = nr * M::L + 3 + (i - nr * SPR);
+    float v = dy0[base];
+    #pragma unroll 4
+    for (int jt = 0; jt < n_times; ++jt) v += dlatent[(size_t)jt * NRL + base];
+    dy0[base] = v;
+  }
+}
+
 // SPLIT_BWD partner wave W + 4: the weight gradients of every stage (mlp_backward_dw), on the
 // exact barrier sequence of bwd_body's critical-path waves (every lds_sync there has its
 // counterpart here, in the same order).

@@ -2,6 +2,7 @@
 // the type-erased registry entry the C-ABI (ude_rk4.hip) dispatches on.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 #include "ude_rk4.h"
 #include "ude_kernels.h"
@@ -63,6 +64,14 @@ struct Ops {
     if constexpr (M::GST)
       HIPCHK(hipFuncSetAttribute((const void*)&ude_gst_dw_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  Gst<M>::LDS));
+    if constexpr (M::FWD_RES) {
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, false, false, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, false, false, false, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, false, true, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
+    }
     done = true;
     return UDE_OK;
   }
@@ -89,6 +98,14 @@ struct Ops {
   static int64_t static_ws_floats(int n_tiles) {
     if (!M::HOIST) return 0;
     return (int64_t)n_tiles * M::K0 * TT + (int64_t)M::STATIC_CHUNKS * M::K0 * M::S16;
+  }
+
+  // the resident-weight forward (one workgroup per CU) when every tile has a CU of its own;
+  // UDE_FWD_RES=0 turns it off (A/B measurement)
+  static bool fwd_res(int n_tiles, int cus) {
+    if constexpr (!M::FWD_RES) return false;
+    static const int env = [] { const char* e = getenv("UDE_FWD_RES"); return e ? atoi(e) : 1; }();
+    return env != 0 && n_tiles <= cus;
   }
 
   // BAYES: one weight sample per RHS evaluation (4 per RK4 step)
@@ -218,6 +235,9 @@ struct Ops {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if (M::SPLIT_FWD && n_tiles <= cus)
       hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD, true>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F_DEC, s, a);
+    else if (fwd_res(n_tiles, cus))
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F_DEC,
+                         s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
@@ -365,6 +385,12 @@ struct Ops {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     if (ckpt && M::SPLIT_FWD && n_tiles <= cus)
       hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F, s, a);
+    else if (fwd_res(n_tiles, cus) && ckpt)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, false, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F,
+                         s, a);
+    else if (fwd_res(n_tiles, cus))
+      hipLaunchKernelGGL((ude_fwd_kernel<M, false, false, false, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F,
+                         s, a);
     else if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());

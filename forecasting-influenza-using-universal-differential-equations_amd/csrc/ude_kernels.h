@@ -280,9 +280,9 @@ struct NoWRegs {
   static constexpr bool ON = false;
   f4 wf[1], wb[1], wx[1];
 };
-template <class M, int W, bool BWD, bool NEED_F_ = !BWD || !M::ACT_STORED>
+template <class M, int W, bool BWD, bool NEED_F_ = !BWD || !M::ACT_STORED, bool FORCE = false>
 struct WRegs {
-  static constexpr bool ON = M::WREG;
+  static constexpr bool ON = M::WREG || FORCE;
   static constexpr bool NEED_F = NEED_F_;   // a stored-activation RK4 backward never runs the forward
   static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
   static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
@@ -370,21 +370,28 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
         constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
         const float* b = rec + inoff + g * (KP / 4);
         // B quads are read in chunks of QB ahead of their MFMAs (one LDS wait per chunk)
-        constexpr int NQ = KP / 16, QB = 5;
-#pragma unroll
-        for (int q0 = 0; q0 < NQ; q0 += QB) {
-          f4 xb[QB];
-          f4 fa[CHUNK_A ? M::FT(d) : 1][CHUNK_A ? QB : 1];
+        constexpr int NQ = KP / 16, QB = CHUNK_A ? 4 : 5;
+        // CHUNK_A: the chunks' weight fragments double-buffered, chunk c + 1's loads in flight
+        // during chunk c's MFMAs (fully unrolled: the buffer index is a constant)
+        f4 fa[2][CHUNK_A ? M::FT(d) : 1][CHUNK_A ? QB : 1];
+        auto load_chunk = [&](int bsel, int c0) {
           if constexpr (CHUNK_A)
             sfor<M::FT(d)>([&](auto kk) {
               constexpr int k = decltype(kk)::value;
               if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net) {
                 constexpr int rt = M::frt(d, k);
 #pragma unroll
-                for (int q = q0; q < q0 + QB && q < NQ; ++q)
-                  fa[k][q - q0] = ldw(rs, lane * 16, (M::wf_off(net, d) + rt * NQ * 256 + q * 256) * 4);
+                for (int q = c0; q < c0 + QB && q < NQ; ++q)
+                  fa[bsel][k][q - c0] = ldw(rs, lane * 16, (M::wf_off(net, d) + rt * NQ * 256 + q * 256) * 4);
               }
             });
+        };
+        load_chunk(0, 0);
+#pragma unroll
+        for (int q0 = 0; q0 < NQ; q0 += QB) {
+          f4 xb[QB];
+          const int cb = (q0 / QB) & 1;
+          if (q0 + QB < NQ) load_chunk(cb ^ 1, q0 + QB);
 #pragma unroll
           for (int q = q0; q < q0 + QB && q < NQ; ++q) xb[q - q0] = *reinterpret_cast<const f4*>(b + 4 * q);
           __builtin_amdgcn_sched_barrier(0);
@@ -397,7 +404,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
                 constexpr int k = decltype(kk)::value;
                 if constexpr (M::fowner(d, k) == W && M::fnet(d, k) == net) {
                   f4 wq;
-                  if constexpr (CHUNK_A) wq = fa[CHUNK_A ? k : 0][CHUNK_A ? q - q0 : 0];
+                  if constexpr (CHUNK_A) wq = fa[cb][CHUNK_A ? k : 0][CHUNK_A ? q - q0 : 0];
                   else wq = FR(M::fq_before(W, d, k) + q);
                   if constexpr (UDE_ABL != 13) acc[k] = mfma4(wq[e], x[e], acc[k]);
                   else acc[k][e] += x[e];
@@ -504,7 +511,11 @@ __device__ __forceinline__ double wave_sum(double v) {
 // lib/VAE.py:138 applies it) and the latent_init_loss sum over y[..., :3] (:189); the training
 // forward also stores the final state for the decoder backward.  Outputs must be grid hits
 // (schedule mode 1; the host checks).
-template <class M, bool TRAIN, int W, bool SPLIT = false, bool DEC = false>
+// RES (deterministic weights too large for two workgroups' registers, launched when the tiles do not
+// outnumber the CUs): one workgroup per CU with every forward fragment resident in VGPRs for the whole
+// launch -- no phase waits on the L2 latency of its weights (the few-tile / strong-scaling shard case,
+// where no second workgroup on the CU hides it).
+template <class M, bool TRAIN, int W, bool SPLIT = false, bool DEC = false, bool RES = false>
 __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
@@ -519,7 +530,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   double* st_reg = reinterpret_cast<double*>(lds + M::REG_LDS_F) + tid;
   if constexpr (DEC) *st_reg = 0.0;
 
-  WRegs<M, W, false> wr;
+  WRegs<M, W, false, true, RES> wr;
   wr.load(rs, lane);
 
   #pragma unroll 1
@@ -804,17 +815,17 @@ __device__ void fwd_sbody(const KArgs& A, float* lds) {
 
 // SPLIT (training, Model::split_fwd, launched when every tile has a CU of its own): 8 waves.
 // DEC: the decoder epilogue (y_hat and latent_init_loss, no latent).
-template <class M, bool TRAIN, bool SPLIT = false, bool DEC = false>
-__global__ __launch_bounds__(SPLIT ? 2 * NTHREADS : NTHREADS, SPLIT ? 1 : 2) void ude_fwd_kernel(KArgs a) {
+template <class M, bool TRAIN, bool SPLIT = false, bool DEC = false, bool RES = false>
+__global__ __launch_bounds__(SPLIT ? 2 * NTHREADS : NTHREADS, (SPLIT || RES) ? 1 : 2) void ude_fwd_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (SPLIT) {
     if (w >= WAVES) { fwd_sbody<M>(a, lds); return; }
   }
-  if (w == 0) fwd_body<M, TRAIN, 0, SPLIT, DEC>(a, lds);
-  else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT, DEC>(a, lds);
-  else if (w == 2) fwd_body<M, TRAIN, 2, SPLIT, DEC>(a, lds);
-  else fwd_body<M, TRAIN, 3, SPLIT, DEC>(a, lds);
+  if (w == 0) fwd_body<M, TRAIN, 0, SPLIT, DEC, RES>(a, lds);
+  else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT, DEC, RES>(a, lds);
+  else if (w == 2) fwd_body<M, TRAIN, 2, SPLIT, DEC, RES>(a, lds);
+  else fwd_body<M, TRAIN, 3, SPLIT, DEC, RES>(a, lds);
 }
 
 // ============================================================================

@@ -368,6 +368,10 @@ struct Model {
   static constexpr int max_wreg_q() { return cmax(cmax(wreg_q(0), wreg_q(1)), cmax(wreg_q(2), wreg_q(3))); }
   static constexpr int WREG_MAX_Q = 56;      // <= 224 VGPRs of resident fragments per wave
   static constexpr bool WREG = !BAYES && max_wreg_q() <= WREG_MAX_Q;
+  // forward-only resident fragments at one workgroup per CU (ude_fwd_kernel RES): <= 96 quads
+  static constexpr int fwd_wreg_q(int w) { return WF_Q(w) + WB_Q(w); }
+  static constexpr bool FWD_RES = !BAYES && !WREG &&
+                                  cmax(cmax(fwd_wreg_q(0), fwd_wreg_q(1)), cmax(fwd_wreg_q(2), fwd_wreg_q(3))) <= 96;
 
   // ---- parameters in torch order (nn.Linear weight (out,in) then bias) ----------------
   static constexpr int param_w_off(int net, int i) {

@@ -101,11 +101,11 @@ struct Ops {
   }
 
   // the resident-weight forward (one workgroup per CU) when every tile has a CU of its own;
-  // UDE_FWD_RES=0 turns it off (A/B measurement)
+  // UDE_FWD_RES=0 turns it off, =2 forces it at any batch (A/B measurement)
   static bool fwd_res(int n_tiles, int cus) {
     if constexpr (!M::FWD_RES) return false;
     static const int env = [] { const char* e = getenv("UDE_FWD_RES"); return e ? atoi(e) : 1; }();
-    return env != 0 && n_tiles <= cus;
+    return env == 2 || (env != 0 && n_tiles <= cus);
   }
 
   // BAYES: one weight sample per RHS evaluation (4 per RK4 step)
@@ -233,11 +233,13 @@ struct Ops {
     a.fa_w = p->fa_w;
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    // the resident-weight forward runs one workgroup per CU (min(n_tiles, cus) <= gf slabs)
+    const bool res = !(M::SPLIT_FWD && n_tiles <= cus) && fwd_res(n_tiles, cus);
+    if (res) gf = n_tiles < cus ? n_tiles : cus;
     if (M::SPLIT_FWD && n_tiles <= cus)
       hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD, true>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F_DEC, s, a);
-    else if (fwd_res(n_tiles, cus))
-      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F_DEC,
-                         s, a);
+    else if (res)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true, M::FWD_RES>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
@@ -383,14 +385,14 @@ struct Ops {
     a.fa_w = p->fa_w;
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const bool res = !(ckpt && M::SPLIT_FWD && n_tiles <= cus) && fwd_res(n_tiles, cus);
+    if (res) gf = n_tiles < cus ? n_tiles : cus;
     if (ckpt && M::SPLIT_FWD && n_tiles <= cus)
       hipLaunchKernelGGL((ude_fwd_kernel<M, true, M::SPLIT_FWD>), dim3(gf), dim3(2 * NTHREADS), M::LDS_F, s, a);
-    else if (fwd_res(n_tiles, cus) && ckpt)
-      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, false, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F,
-                         s, a);
-    else if (fwd_res(n_tiles, cus))
-      hipLaunchKernelGGL((ude_fwd_kernel<M, false, false, false, M::FWD_RES>), dim3(n_tiles), dim3(NTHREADS), M::LDS_F,
-                         s, a);
+    else if (res && ckpt)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, false, M::FWD_RES>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
+    else if (res)
+      hipLaunchKernelGGL((ude_fwd_kernel<M, false, false, false, M::FWD_RES>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     else if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());

@@ -79,6 +79,23 @@ def macs_per_eval(w):
     return tot
 
 
+def executed_macs_per_eval(w):
+    """Multiply-adds the MFMA tiles actually issue per evaluation: every layer padded to 16 rows /
+    16 input columns, layer 0 over the 3R dynamic features only for the deterministic kernels (the
+    static latent dims' contribution is hoisted once per tile, ude_kernels.h static_hoist), over
+    [dynamic | static] for the Bayesian ones."""
+    R, L = w["R"], w["L"]
+    p16 = lambda x: (x + 15) // 16 * 16
+    in0 = p16(3 * R) + (p16(R * (L - 3)) if w["kind"].startswith("Bayes_") else 0)
+    tot = 0
+    for sizes, out in ((w["net"], 2 * R), (w["aug"], 3 * R)):
+        if sizes is None:
+            continue
+        dims = [in0] + [p16(x) for x in sizes] + [p16(out)]
+        tot += sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    return tot
+
+
 def make_t(spec):
     kind, n, div = spec
     return torch.arange(n, dtype=torch.float32) / div
@@ -576,7 +593,12 @@ def main():
                          "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
                          "traffic": pmc, "traffic_source": PMC_SOURCE.get(args.workload + "_bwd"),
                          "avg_launch_ms": kms["bwd"],
-                         "algorithmic_flop_per_launch": bwd_flop_launch},
+                         "algorithmic_flop_per_launch": bwd_flop_launch,
+                         # the MFMA work the kernel issues (padded tiles, hoisted static features) per
+                         # algorithmic MAC, and the MFMA pipe's busy fraction that implies
+                         "executed_per_algorithmic_mac": executed_macs_per_eval(w) / macs_per_eval(w),
+                         "executed_mac_frac": ((achieved / PEAK_FP32_TFLOPS) * executed_macs_per_eval(w)
+                                               / macs_per_eval(w)) if achieved else None},
             "kernels": {"fwd_ms": kms["fwd"], "bwd_ms": kms["bwd"],
                         "fwd_tflops": fwd_flop_launch / (kms["fwd"] * 1e-3) / 1e12 if kms["fwd"] else None,
                         "step_tflops_algorithmic": value * flop_unit / 1e12,

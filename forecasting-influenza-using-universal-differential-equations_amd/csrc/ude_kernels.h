@@ -287,7 +287,7 @@ struct WRegs {
   static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
   static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
   f4 wf[NF > 0 ? NF : 1], wb[NB > 0 ? NB : 1], wx[NX > 0 ? NX : 1];
-  __device__ __forceinline__ void load(Rsrc rs, int lane) {
+  __device__ __forceinline__ void load(Rsrc rs, int lane, bool wait = true) {
     if constexpr (ON) {
       const int g = lane >> 4;
       sfor<M::D>([&](auto dd) {
@@ -307,7 +307,7 @@ struct WRegs {
       // wait for the fragments here, once: the loop-carried wait analysis otherwise keeps them
       // "pending" at the step loop's head and puts a vmcnt(0) before the first MFMA of every
       // stage, which also drains the loads prefetched a stage ahead (s_waitcnt vmcnt(0))
-      __builtin_amdgcn_s_waitcnt(0x0F70);
+      if (wait) __builtin_amdgcn_s_waitcnt(0x0F70);
     }
   }
 };
@@ -530,8 +530,12 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   double* st_reg = reinterpret_cast<double*>(lds + M::REG_LDS_F) + tid;
   if constexpr (DEC) *st_reg = 0.0;
 
-  WRegs<M, W, false, true, RES> wr;
-  wr.load(rs, lane);
+  // BAYES at small sizes (PFB): each evaluation's weight sample lives in registers, loaded while the
+  // previous evaluation's flux pass runs (its L2 latency off the layer phases; at one tile per CU
+  // nothing else on the CU hides it)
+  constexpr bool PFB = M::FWD_PFB;
+  WRegs<M, W, false, true, RES || PFB> wr;
+  if constexpr (!PFB) wr.load(rs, lane);
 
   #pragma unroll 1
   for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
@@ -623,7 +627,14 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         // BAYES: evaluation 4 step + j has its own weight sample
         Rsrc rse = rs;
         if constexpr (M::BAYES) rse = make_rsrc(A.pack + (size_t)(4 * step + j) * M::PACK_TOTAL, M::PACK_TOTAL * 4);
+        if constexpr (PFB) {
+          if (step == 0 && j == 0) wr.load(rse, lane, false);        // the tile's first evaluation
+        }
         mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
+        if constexpr (PFB) {
+          const int en = 4 * step + j + 1;
+          if (en < 4 * A.n_steps) wr.load(make_rsrc(A.pack + (size_t)en * M::PACK_TOTAL, M::PACK_TOTAL * 4), lane, false);
+        }
         if constexpr (TRAIN && M::ACT_STORED && !SPLIT && UDE_ABL != 11) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)

@@ -372,6 +372,10 @@ struct Model {
   static constexpr int fwd_wreg_q(int w) { return WF_Q(w) + WB_Q(w); }
   static constexpr bool FWD_RES = !BAYES && !WREG &&
                                   cmax(cmax(fwd_wreg_q(0), fwd_wreg_q(1)), cmax(fwd_wreg_q(2), fwd_wreg_q(3))) <= 96;
+  // Bayesian forward with few fragments per wave: each evaluation's sample in registers, prefetched
+  // during the previous evaluation's flux pass (fwd_body PFB)
+  static constexpr bool FWD_PFB = BAYES &&
+                                  cmax(cmax(fwd_wreg_q(0), fwd_wreg_q(1)), cmax(fwd_wreg_q(2), fwd_wreg_q(3))) <= 40;
 
   // ---- parameters in torch order (nn.Linear weight (out,in) then bias) ----------------
   static constexpr int param_w_off(int net, int i) {

@@ -203,7 +203,7 @@ struct Model {
   // run that path; waves 4-7 accumulate the weight gradients of the same phase (which nothing
   // in the stage waits for) from the same LDS operands, on the same SIMDs, so their MFMAs fill
   // the critical path's gaps.
-  static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !BAYES;
+  static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !GST;
   // Large records (STORE_ACT_D) split the same way (SPLIT_BWD_L): waves 4-7 (bwd_wbody_l) hold the
   // weight-gradient accumulators (the ~176 VGPRs per wave that kept the 4-wave kernel at one wave per
   // SIMD) and move the next stage's data with LDS-DMA (global_load_lds): each layer's activation rows
@@ -218,7 +218,7 @@ struct Model {
   // Backward critical path without weight-gradient accumulators (GST; SPLIT_BWD_L's waves 0-3) and
   // weights read from L2 (never register-resident at these sizes): each phase's input-gradient fragments are loaded one phase
   // ahead (the first phase's before the flux pass), so no phase waits on the L2 latency
-  static constexpr bool PF_X = GST || SPLIT_BWD_L;
+  static constexpr bool PF_X = GST || SPLIT_BWD_L || BAYES;
   static constexpr int BWD_THREADS = SPLITB ? 2 * NTHREADS : NTHREADS;
   // Training forward of small records at one tile per CU: four more waves copy each stage's
   // activation rows from the record to HBM during the flux pass, off the critical path

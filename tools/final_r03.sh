@@ -28,4 +28,6 @@ python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write state49 > $O/pmc_summary.
 cp profiles/pmc_state49_*.json $O/ 2>/dev/null || true
 timeout -k 10 120 python -u tools/stage_profile.py state49 > $O/stage_state49.txt 2>&1 || exit 23
 timeout -k 10 120 python -u tools/stage_profile.py us_northstar > $O/stage_m1.txt 2>&1 || exit 24
+timeout -k 10 120 python -u tools/stage_profile.py us_fp32 > $O/stage_m1_fp32.txt 2>&1 || exit 25
+timeout -k 10 120 python -u tools/stage_profile.py bayes_state49 > $O/stage_bayes49.txt 2>&1 || exit 26
 exit 0

@@ -1692,7 +1692,7 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
     constexpr bool GST_A = M::GST && M::STORE_ACT_D;
     f4 actg[GST_A ? act_q_per_thread<M>() : 1];
     float gvg[GST_A ? SL : 1][3];          // GST: the next step's output cotangents, loaded a stage ahead
-    f4 fxp[M::PF_X ? M::WX_Q(W) : 1];
+    f4 fxp[(M::PF_X && M::WX_Q(W) > 0) ? M::WX_Q(W) : 1];
     for (int step = A.n_steps - 1; step >= 0; --step) {
       const float dt = sc.dt[step];
       // step start: RK_A already holds the adjoint of y_{n+1} including this step's

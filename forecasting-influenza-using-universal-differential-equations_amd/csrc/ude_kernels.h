@@ -1174,87 +1174,12 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
 // d the rows the wave owns: dW += g . in^T (MFMA, K = the tile's 16 trajectories) from the
 // phase's LDS operands, and per-trajectory bias sums in registers (reduced over the trajectories
 // once, at the launch end, instead of a cross-lane reduction every phase).
-// BAYES (es = this evaluation's eps in slab order): each tile's evaluation contribution is formed on
-// its own and added to the plain and the eps-weighted accumulator (dws); the bias rows are reduced
-// over the tile's trajectories every phase (their eps weighting is per evaluation) into the LDS row
-// sums DB / DBS -- the same arithmetic as mlp_backward's non-split Bayesian path.
-// eps of phase d for wave W (dW tiles in C layout, bias rows) into the caller's per-stage arrays
-template <class M, int W, int d>
-__device__ __forceinline__ void load_eps(Rsrc es, int lane, f4* efp, f4* ebp) {
-  const int g = lane >> 4;
-  sfor<M::FT(d)>([&](auto kk) {
-    constexpr int k = decltype(kk)::value;
-    if constexpr (M::fowner(d, k) == W) {
-      constexpr int e0 = M::ndw_before(W, d, k);
-      sfor<M::rti(M::fnet(d, k), d)>([&](auto cc) {
-        constexpr int ct = decltype(cc)::value;
-        efp[e0 + ct] = ldw(es, lane * 16, (M::dyn_tiles_before(d, k) + ct) * 1024);
-      });
-      ebp[M::ng_before(W, d, k)] = ldw(es, g * 16, (M::SLAB_DB + (M::FTbase(d) + k) * 16) * 4);
-    }
-  });
-}
-
-// BAYES: efp / ebp ([NDW(W)] / [NG(W)] quads) hold the stage's eps, each phase's loaded one phase
-// ahead (the caller issues the first phase's at the stage start), so no phase of these waves waits
-// on the L2 latency of its eps (every barrier of the stage waited for it).
 template <class M, int W, int SR>
-__device__ __forceinline__ void mlp_backward_dw(float* lds, f4* dw, f4* g0t, f4* gacc, int lane, Rsrc es,
-                                                f4* dws = nullptr, f4* efp = nullptr, f4* ebp = nullptr) {
+__device__ __forceinline__ void mlp_backward_dw(const float* lds, f4* dw, f4* g0t, f4* gacc, int lane) {
   const int t = lane & 15, g = lane >> 4;
   const float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
     constexpr int d = M::D - 1 - decltype(ee)::value;
-    if constexpr (M::BAYES) {
-      auto ef = [&](int i) { return efp[M::ndw_before(W, d, 0) + i]; };
-      sfor<M::FT(d)>([&](auto kk) {
-        constexpr int k = decltype(kk)::value;
-        if constexpr (M::fowner(d, k) == W) {
-          constexpr int net = M::fnet(d, k), rt = M::frt(d, k), goff = M::gbuf(net, d);
-          constexpr int inoff = d == 0 ? M::Y_OFF : M::act_off(net, d - 1);
-          constexpr int NC = M::rti(net, d);
-          const f4 gv = *reinterpret_cast<const f4*>(rec + goff + rt * 16 + g * 4);
-          float ga[4], bv[4][NC];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            ga[s] = lds[(4 * g + s) * SR + goff + rt * 16 + t];
-#pragma unroll
-            for (int ct = 0; ct < NC; ++ct) bv[s][ct] = lds[(4 * g + s) * SR + inoff + ct * 16 + t];
-          }
-          f4 tmp[NC];
-          sfor<NC>([&](auto cc) { tmp[decltype(cc)::value] = f4zero(); });
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            sfor<NC>([&](auto cc) {
-              constexpr int ct = decltype(cc)::value;
-              tmp[ct] = mfma4(ga[s], bv[s][ct], tmp[ct]);
-            });
-          sfor<NC>([&](auto cc) {
-            constexpr int ct = decltype(cc)::value;
-            constexpr int idx = M::ndw_before(W, d, k) + ct;
-            constexpr int e0 = M::ndw_before(W, d, k) - M::ndw_before(W, d, 0);
-            dw[idx] += tmp[ct];
-            dws[idx] += tmp[ct] * ef(e0 + ct);
-          });
-          f4 r = gv;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-            r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-          }
-          if (t == 0) {
-            float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
-            float* dbs = lds + M::DBS_LDS + (M::FTbase(d) + k) * 16 + g * 4;
-            const f4 e = ebp[M::ng_before(W, d, k)];
-            db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
-            dbs[0] += r[0] * e[0]; dbs[1] += r[1] * e[1]; dbs[2] += r[2] * e[2]; dbs[3] += r[3] * e[3];
-          }
-        }
-      });
-      if constexpr (d > 0) load_eps<M, W, d - 1>(es, lane, efp, ebp);
-      lds_sync();
-      return;
-    }
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W && !(UDE_ABL == 6 && d == 1)) {
@@ -1603,10 +1528,10 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   // SPLITB: the weight-gradient accumulators live on the partner waves (bwd_wbody / bwd_wbody_l)
   // GST: no weight-gradient accumulators (ude_gst_dw_kernel forms them from the stored rows)
   constexpr bool NO_DW = M::SPLITB || M::GST;
-  f4 dw[NO_DW ? 1 : NDWn], dws[(M::BAYES && !NO_DW) ? NDWn : 1], g0t[NZn], c1[NZn];
+  f4 dw[NO_DW ? 1 : NDWn], dws[(M::BAYES && !M::GST) ? NDWn : 1], g0t[NZn], c1[NZn];
 #pragma unroll
   for (int i = 0; i < (NO_DW ? 1 : NDWn); ++i) dw[i] = f4zero();
-  if constexpr (M::BAYES && !NO_DW) {
+  if constexpr (M::BAYES && !M::GST) {
 #pragma unroll
     for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
   }
@@ -2094,14 +2019,9 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
   constexpr int NGn = M::NG(W) > 0 ? M::NG(W) : 1;
   const int lane = threadIdx.x & 63, t16 = lane & 15, g = lane >> 4;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
-  f4 dw[NDWn], dws[M::BAYES ? NDWn : 1], g0t[NZn], gacc[NGn];
-  f4 efp[M::BAYES ? NDWn : 1], ebp[M::BAYES ? NGn : 1];     // BAYES: the stage's eps (one phase ahead)
+  f4 dw[NDWn], g0t[NZn], gacc[NGn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
-  if constexpr (M::BAYES) {
-#pragma unroll
-    for (int i = 0; i < NDWn; ++i) dws[i] = f4zero();
-  }
 #pragma unroll
   for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
   lds_sync();                            // record zeroed
@@ -2172,28 +2092,20 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
         if (jj == 1 && step > 0) out_issue<M>(A, sc, step - 1, n0, gvc, wt);
         have = nstep >= 0;
         if (have) get_stage(tile, nstep, njj);
-        // BAYES: this evaluation's eps, the first phase's now (its latency under the flux pass)
-        Rsrc esr = make_rsrc(A.pack, 0);
-        if constexpr (M::BAYES) {
-          esr = make_rsrc(A.eslab + (size_t)(4 * step + jj) * M::SLAB_TOTAL, M::SLAB_TOTAL * 4);
-          load_eps<M, W, M::D - 1>(esr, lane, efp, ebp);
-        }
         lds_sync();                      // flux pass: final-layer gradients written
         if constexpr (UDE_ABL == 1) { sfor<M::D>([&](auto) { lds_sync(); }); }
-        else if constexpr (M::BAYES)
-          mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane, esr, dws, efp, ebp);
-        else mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane, make_rsrc(A.pack, 0));
+        else mlp_backward_dw<M, W, SR>(lds, dw, g0t, gacc, lane);
       }
     }
     lds_sync();                          // tile end: dy0
     lds_sync();
-    if constexpr (!M::BAYES) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
+    g0_tile_end<M, W>(A, lds, g0t, tile, lane);
     lds_sync();
   }
   // kernel end: dW tiles -> slab; bias row sums of layers >= 1 from the per-trajectory sums
-  // (BAYES: the bias rows were reduced per evaluation)
-  dw_to_slab<M, W>(dw, dws, myslab, lane);
-  if constexpr (!M::BAYES) sfor<M::D>([&](auto dd) {
+  f4 none[1];
+  dw_to_slab<M, W>(dw, none, myslab, lane);
+  sfor<M::D>([&](auto dd) {
     constexpr int d = decltype(dd)::value;
     if constexpr (d > 0) sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -2348,7 +2260,7 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_B;
   constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
   constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
-  const int lane = threadIdx.x & 63;
+  int lane = threadIdx.x & 63;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
   f4 dw[NDWn], g0t[NZn];
 #pragma unroll
@@ -2386,6 +2298,10 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
       for (int jj = 3; jj >= 0; --jj) {
         const int nstep = jj > 0 ? step : step - 1, njj = jj > 0 ? jj - 1 : 3;
         const bool have = nstep >= 0;
+        // lane is opaque per stage: the ~40 lane-derived LDS addresses of the stage (staging copy,
+        // operand reads) are recomputed here instead of hoisted out of the loop, where they spilled
+        // next to the 176 dW VGPRs and every scratch reload (a vmcnt wait) drained the DMAs in flight
+        asm volatile("" : "+v"(lane));
         wait_dma();                                     // this stage's rows and input have landed
         put_stage();
         lds_sync_dma();                                 // stage input + activation rows in the record

@@ -202,8 +202,10 @@ struct Model {
   // critical path (flux -> input gradients layer by layer -> RK adjoint) exposed.  Waves 0-3
   // run that path; waves 4-7 accumulate the weight gradients of the same phase (which nothing
   // in the stage waits for) from the same LDS operands, on the same SIMDs, so their MFMAs fill
-  // the critical path's gaps.
-  static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !GST;
+  // the critical path's gaps.  Not for Bayes: the partner waves would hold the plain and the
+  // eps-weighted dW (2 x 128 VGPRs at [64,64,32]) and spill (measured M1 bwd 21.2 ms vs 12.4 ms for
+  // the 4-wave kernel at one wave per SIMD).
+  static constexpr bool SPLIT_BWD = STORE_ACT && SLOTS_ == 1 && !BAYES;
   // Large records (STORE_ACT_D) split the same way (SPLIT_BWD_L): waves 4-7 (bwd_wbody_l) hold the
   // weight-gradient accumulators (the ~176 VGPRs per wave that kept the 4-wave kernel at one wave per
   // SIMD) and move the next stage's data with LDS-DMA (global_load_lds): each layer's activation rows
@@ -215,9 +217,10 @@ struct Model {
   static constexpr bool SPLIT_BWD_L = false;
 #endif
   static constexpr bool SPLITB = SPLIT_BWD || SPLIT_BWD_L;
-  // Backward critical path without weight-gradient accumulators (GST; SPLIT_BWD_L's waves 0-3) and
-  // weights read from L2 (never register-resident at these sizes): each phase's input-gradient fragments are loaded one phase
-  // ahead (the first phase's before the flux pass), so no phase waits on the L2 latency
+  // Backward critical path with weights read from L2 (GST; SPLIT_BWD_L's waves 0-3; every Bayesian
+  // backward, whose per-evaluation samples are never register-resident): each phase's input-gradient
+  // fragments are loaded one phase ahead (the first phase's before the flux pass), so no phase waits
+  // on the L2 latency (Bayes M1 bwd 13.4 -> 12.4 ms)
   static constexpr bool PF_X = GST || SPLIT_BWD_L || BAYES;
   static constexpr int BWD_THREADS = SPLITB ? 2 * NTHREADS : NTHREADS;
   // Training forward of small records at one tile per CU: four more waves copy each stage's

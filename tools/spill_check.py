@@ -36,6 +36,19 @@ def one(ic):
     return configs.config_key(c), open(os.path.join(d, "k.s")).read(), ""
 
 
+def scratch_ops(txt):
+    """scratch load / store instructions per kernel symbol (a private segment without any is an
+    unused private array, not a spill)"""
+    ops, cur = {}, None
+    for ln in txt.split("\n"):
+        m = re.match(r"^(_Z\S+):", ln)
+        if m:
+            cur = m.group(1)
+        elif cur and "scratch_" in ln and not ln.lstrip().startswith(";"):
+            ops[cur] = ops.get(cur, 0) + 1
+    return ops
+
+
 bad = 0
 with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
     for key, txt, err in ex.map(one, sel):
@@ -43,15 +56,17 @@ with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
             print(f"{key}: BUILD FAILED\n{err}")
             bad += 1
             continue
+        ops = scratch_ops(txt)
         for blk in re.findall(r"\n\s+- \.agpr_count:.*?(?=\n\s+- \.agpr_count:|\n\.end_amdgpu_metadata)", txt, re.S):
             f = dict(re.findall(r"\.(\w+):\s+(\S+)", blk))
             name = f.get("name", "?")
             scratch = int(f.get("private_segment_fixed_size", "0"))
             short = re.sub(r"ude::Model<[^>]*>", "M", subprocess.run(["c++filt"], input=name, capture_output=True,
                                                                      text=True).stdout.strip())[:90]
-            if scratch > 0:
+            nops = ops.get(name, 0)
+            if scratch > 0 and nops > 0:
                 bad += 1
-                print(f"SPILL {key:34s} scratch {scratch:5d} vgpr {f.get('vgpr_count')} {short}")
+                print(f"SPILL {key:34s} scratch {scratch:5d} B {nops:4d} ops vgpr {f.get('vgpr_count')} {short}")
             elif "ude_bwd_kernel" in name or "ude_fwd_kernel" in name:
                 print(f"      {key:34s} vgpr {f.get('vgpr_count'):>4} agpr {f.get('agpr_count'):>4} {short}")
 print("spilling kernels / failed builds:", bad)

@@ -126,7 +126,8 @@ template <class M, int MODE, int W>
 __device__ void dopri_body(const DArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
-  const int tid = threadIdx.x, lane = tid & 63;
+  int tid = threadIdx.x;
+  const int lane = tid & 63;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   const DopriCtl* C = A.ctl;
@@ -233,6 +234,7 @@ __device__ void dopri_body(const DArgs& A, float* lds) {
     constexpr int NST = MODE == dp::MODE_STEP ? 6 : 1;
     #pragma unroll 1
     for (int s = 0; s < NST; ++s) {
+      asm volatile("" : "+v"(tid));
       mlp_forward<M, W, SR>(rs, lds, c1, lane);
       sfor<SL>([&](auto ss) {
         constexpr int sl = decltype(ss)::value;

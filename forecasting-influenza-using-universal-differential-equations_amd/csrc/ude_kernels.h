@@ -519,7 +519,8 @@ template <class M, bool TRAIN, int W, bool SPLIT = false, bool DEC = false, bool
 __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int SL = M::SLOTS;
-  const int tid = threadIdx.x, lane = tid & 63;
+  int tid = threadIdx.x;
+  const int lane = tid & 63;
   const Sched sc(A.sched, A.n_steps, A.n_out);
   const size_t NRL = (size_t)A.n_traj * M::R * M::L;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
@@ -622,6 +623,10 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     if constexpr (DEC) dec_emit(0);               // output 0 = y0
 
     for (int step = 0; step < A.n_steps; ++step) {
+      // DEC (R=49, at the 256-VGPR limit): the thread-derived 64-bit store addresses are recomputed
+      // each step rather than hoisted out of the loop and spilled (each reload waited on every
+      // checkpoint / activation store in flight)
+      if constexpr (DEC) asm volatile("" : "+v"(tid));
       const float dt = sc.dt[step];
       for (int j = 0; j < 4; ++j) {
         // BAYES: evaluation 4 step + j has its own weight sample

@@ -62,6 +62,12 @@ WORKLOADS = {
     "bayes_state49": dict(_STATE, kind="Bayes_FaFp", n_traj=64 * 10 * 32, t=("arange", 9, 1.0),
                           desc="Bayesian state model (models_bayes.py Bayes_FaFp, run_ode.py 'UONNb'), R=49, "
                                "64 MC samples x 10 seasons x 32 windows, 8 weekly RK4 steps"),
+    "state49_fp": dict(kind="Fp", R=49, L=8, net=[64, 64, 32], aug=None, n_traj=64 * 10 * 32, t=("arange", 9, 1.0),
+                       desc="state model R=49, rate net only (run_ode.py 'Fp' variant), 20,480 trajectories, "
+                            "8 weekly RK4 steps (development line: --workload)"),
+    "state49_fa": dict(kind="Fa", R=49, L=8, net=None, aug=[64, 64], n_traj=64 * 10 * 32, t=("arange", 9, 1.0),
+                       desc="state model R=49, augmentation net only (run_ode.py 'Fa' variant), 20,480 "
+                            "trajectories, 8 weekly RK4 steps (development line: --workload)"),
     "tiny": dict(_US, n_traj=64, t=("arange", 5, 1.0),
                  desc="plumbing rehearsal only (CPU / gloo): US model, 64 trajectories, 4 weekly steps"),
 }

@@ -639,9 +639,16 @@ def main():
         print("[bench] cpu baselines", file=sys.stderr, flush=True)
         res["cpu_baseline"] = cpu_baseline(w, mod, threads=CPU_THREADS)
         res["cpu_baseline_1thread"] = cpu_baseline(w, mod, threads=1)
+        # BASELINE.md section 3 / SURVEY 8d: the north-star M1 models too (FaFp and Fp [32, 32], R = 1)
+        for name, wl in (("cpu_baseline_M1", "us_northstar"), ("cpu_baseline_M1_fp32", "us_fp32")):
+            wm = WORKLOADS[wl]
+            m_cpu, _, _, _ = build(pkg, wm, torch.device("cpu"), seed=1000)
+            res[name] = {"workload": wl, "threads_16": cpu_baseline(wm, m_cpu, threads=CPU_THREADS),
+                         "threads_1": cpu_baseline(wm, m_cpu, threads=1)}
         if (os.cpu_count() or 1) > CPU_THREADS:
-            # also at every visible host core (more than this box's share per GPU)
-            res["cpu_baseline_all_visible_cores"] = cpu_baseline_child(args.workload, os.cpu_count())
+            # also at more host cores than this box's share per GPU (capped at 64 threads:
+            # at every visible core, 256 here, the shared host stalls for minutes)
+            res["cpu_baseline_many_cores"] = cpu_baseline_child(args.workload, min(os.cpu_count(), 64))
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

@@ -243,7 +243,7 @@ struct Ops {
     else hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, stats_out);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(ude_sum_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)reg_slab, gf, reg_out);
     HIPCHK(hipGetLastError());
@@ -397,7 +397,7 @@ struct Ops {
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)stats_slab, gf, n_eval, stats_out);
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, stats_out);
     HIPCHK(hipGetLastError());
     return UDE_OK;
   }
@@ -587,7 +587,7 @@ struct DopriOps {
     hipLaunchKernelGGL((ude_dopri_kernel<M, dp::MODE_STEP>), g, b, M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
     const double n_eval = (double)h.n_evals * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, (const double*)a.stats_slab, grid,
+    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, a.stats_slab, grid,
                        n_eval, stats_out);
     HIPCHK(hipGetLastError());
     return UDE_OK;

@@ -2728,8 +2728,9 @@ __global__ void ude_sum_finalize_kernel(const double* __restrict__ part, int n, 
 }
 
 template <int V_ = 0>
-__global__ void ude_stats_finalize_kernel(const double* __restrict__ slab, int ngrid, double n_eval,
+__global__ void ude_stats_finalize_kernel(double* __restrict__ slab, int ngrid, double n_eval,
                                           float* __restrict__ out) {
+  // ... and the fp64 totals back into slab[0..4] (read by the data-parallel statistics exchange)
   // wave c sums statistic c: lane-strided partials, then a fixed butterfly (deterministic)
   __shared__ double tot[5];
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
@@ -2749,6 +2750,7 @@ __global__ void ude_stats_finalize_kernel(const double* __restrict__ slab, int n
     out[2 + c] = (float)sqrt(var > 0.0 ? var : 0.0);
   }
   if (c == 4) out[4] = (float)sqrt(tot[4]);
+  if (c < 5) slab[c] = tot[c];
 }
 
 }  // namespace ude

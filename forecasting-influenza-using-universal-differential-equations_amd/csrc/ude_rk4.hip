@@ -226,7 +226,8 @@ void ude_debug_set_prof(unsigned long long* p) { ude::g_prof_buffer = p; }
 #endif
 
 const char* ude_build_info(void) {
-  return "ude_rk4 gfx950: v_mfma_f32_16x16x4_f32, TT=16, 4 waves/WG, registry=" UDE_REGISTRY_TAG;
+  return "ude_rk4 gfx950: v_mfma_f32_16x16x4_f32, TT=16, 4 waves/WG, registry=" UDE_REGISTRY_TAG
+         " src=" UDE_SRC_HASH " extra_flags=[" UDE_EXTRA_FLAGS "]";
 }
 
 }  // extern "C"

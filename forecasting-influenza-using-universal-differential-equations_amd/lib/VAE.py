@@ -136,19 +136,31 @@ class VAE:
         each batch's windows over the ranks (see the module docstring)."""
         self._dp = {"group": group, "world": udist.world_size(group), "rank": udist.rank(group)}
         udist.broadcast_parameters(self.parameters(), group=group)
+        # every rank then draws the same full-batch eps each step (__call__ slices its shard)
+        udist.broadcast_rng_state(self.device, group=group)
         return self
 
     def _shard(self, B):
         """This rank's contiguous window range [lo, hi) of a B-window batch."""
         world, rank = self._dp["world"], self._dp["rank"]
+        if B < world:
+            # an empty shard would reach the solve with no trajectories while the peers wait in
+            # the statistics / gradient all-reduces
+            raise ValueError(f"data-parallel train_step: a batch of {B} windows cannot be sharded over "
+                             f"{world} ranks (need at least one window per rank)")
         base, rem = divmod(B, world)
         lo = rank * base + min(rank, rem)
         return lo, lo + base + (1 if rank < rem else 0)
     def __call__(self, x, t, n_samples=32, training=False):
         B = x.shape[0]
+        # release the previous call's training store (LazyLatent keeps the stage checkpoints and
+        # stored activations alive) before this call's solve allocates its own
+        self.__dict__["_latent"] = None
+        self._pred_src = None
         if self._dp_eps is not None:
-            # sharded step: the full batch's eps (same draw on every rank) sliced to this shard, so
-            # the data-parallel step sees exactly the single-process step's samples
+            # sharded step: the full batch's eps sliced to this shard.  Every rank's generator
+            # holds rank 0's state (enable_data_parallel) and draws the same count per step, so
+            # the draw is the same on every rank and equals the single-process step's samples
             b_full, lo, hi = self._dp_eps
             eps = torch.randn(n_samples, b_full, self.n_regions, self.ld_enc, dtype=self.dtype,
                               device=self.device)[:, lo:hi]

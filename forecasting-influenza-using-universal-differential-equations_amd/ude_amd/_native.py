@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes
 import hashlib
 import os
+import re
 import shutil
 import subprocess
 import threading
@@ -89,6 +90,10 @@ def make_desc(cfg: _cfgs.Config) -> UdeModelDesc:
 
 class UdeError(RuntimeError):
     pass
+
+
+class UdeStaleLibrary(UdeError):
+    """The prebuilt library does not match the sources in the tree."""
 
 
 def check(rc: int, what: str) -> None:
@@ -302,6 +307,24 @@ def _run(cmd: List[str]) -> None:
         raise UdeError("build command failed:\n" + " ".join(cmd) + "\n" + r.stdout[-8000:])
 
 
+def source_hash() -> str:
+    """sha1 (16 hex digits) of every source the library is compiled from (csrc/*.h, csrc/*.hip,
+    include/ude_rk4.h) and of the compile flags.  Embedded in ``ude_build_info`` so a prebuilt
+    library that no longer matches the tree is refused at load (``prebuilt``)."""
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
+    srcs.append(os.path.join(INCLUDE, "ude_rk4.h"))
+    h = hashlib.sha1()
+    for f in srcs:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(HIP_FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+_INFO_HASH = re.compile(r"\bsrc=([0-9a-f]+)")
+
+
 def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: Optional[int] = None,
                   extra_flags: Sequence[str] = ()) -> str:
     """Compile one object per configuration + the C-ABI, link into out_path."""
@@ -315,6 +338,8 @@ def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: O
     reg.append(f"constexpr int kNumEntries = {len(cfgs)};")
     reg.append("}  // namespace ude")
     reg.append(f'#define UDE_REGISTRY_TAG "{tag}:{len(cfgs)}"')
+    reg.append(f'#define UDE_SRC_HASH "{source_hash()}"')
+    reg.append(f'#define UDE_EXTRA_FLAGS "{" ".join(extra_flags)}"')
     with open(os.path.join(gen, "ude_registry.inc"), "w") as f:
         f.write("\n".join(reg) + "\n")
     inc = ["-I", INCLUDE, "-I", CSRC, "-I", gen, *extra_flags]
@@ -357,17 +382,27 @@ def _load(path: str) -> NativeLib:
         return _loaded[path]
 
 
+def built_hash(lib: NativeLib) -> Optional[str]:
+    m = _INFO_HASH.search(lib.build_info())
+    return m.group(1) if m else None
+
+
 def prebuilt() -> NativeLib:
+    """The in-tree prebuilt library; refused if it was built from other sources than the tree's
+    (a stale binary would silently run old kernels)."""
     if not os.path.exists(PREBUILT_LIB):
         raise UdeError(f"{PREBUILT_LIB} is missing: run __graft_entry__.build() (hipcc, gfx950)")
-    return _load(PREBUILT_LIB)
+    lib = _load(PREBUILT_LIB)
+    got, want = built_hash(lib), source_hash()
+    if got != want:
+        raise UdeStaleLibrary(f"{PREBUILT_LIB} is stale (built from sources {got}, tree is {want}): "
+                       "rebuild it with __graft_entry__.build()")
+    return lib
 
 
 def jit_library(cfg: _cfgs.Config) -> NativeLib:
     key = _cfgs.config_key(cfg)
-    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
-    srcs.append(os.path.join(INCLUDE, "ude_rk4.h"))
-    h = hashlib.sha1(b"".join(open(f, "rb").read() for f in srcs)).hexdigest()[:10]
+    h = source_hash()[:10]
     path = os.path.join(JIT_DIR, f"libude_rk4_{key}_{h}.so")
     if not os.path.exists(path):
         os.makedirs(JIT_DIR, exist_ok=True)
@@ -401,6 +436,8 @@ def config_supported(cfg: _cfgs.Config) -> bool:
         try:
             library_for(cfg)
             hit = True
+        except UdeStaleLibrary:
+            raise
         except UdeError:
             hit = False
         _SUPPORTED[cfg] = hit

@@ -76,9 +76,9 @@ def solve_decode(ode, y0: torch.Tensor, t: torch.Tensor, step_size, linear: torc
     params = []
     for lin in ode.ude_linears():
         params += [lin.weight, lin.bias]
-    yhat, reg, stats, token, ckpt = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight, linear.bias,
-                                                            *params)
-    ode._record_fused(stats, plan.n_eval)
+    yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight,
+                                                                  linear.bias, *params)
+    ode._record_fused(stats, plan.n_eval, sums=sums)
     return yhat, reg, LazyLatent(token, ckpt, y0, plan), plan
 
 

@@ -6,11 +6,14 @@ sample statistics of ``nll_loss`` stay local).  Two exchanges are real:
 
 1. forward: the posterior over *all* recorded rates and the Fa norm are
    global (lib/models.py:152-156, lib/VAE.py:180).  Each rank's fused solve
-   yields (mean, std, |Fa|) over its shard; ``sync_side_stats`` turns them into
-   sufficient statistics (n*mean, (n-1)*std^2 + n*mean^2, |Fa|^2), all-reduces
-   those 5 numbers and rebuilds the global (mean, std, |Fa|).  The all-reduce
-   is differentiable (its backward all-reduces the cotangent), so every rank's
-   kernel receives d loss_total / d stats in its backward.
+   leaves its fp64 totals (n, sum b, sum g, sum b^2, sum g^2, sum Fa^2) in the
+   stats slab; ``sync_side_stats`` all-reduces those 6 doubles and forms the
+   global (mean, std, |Fa|) as the kernel's finaliser does.  The all-reduce is
+   differentiable (its backward all-reduces the cotangent; ``fused.stat_sums``
+   maps it onto the kernel's (d mean, d std, d |Fa|) input), so every rank's
+   kernel receives d loss_total / d stats in its backward.  Entries without
+   fp64 totals (eager evaluations) go through sufficient statistics rebuilt
+   from (n, mean, std, |Fa|).
 2. backward: one bucketed all-reduce of the flat parameter gradients.
 """
 from __future__ import annotations
@@ -81,6 +84,22 @@ def broadcast_parameters(params: Iterable[torch.nn.Parameter], src: int = 0, gro
             off += n
 
 
+def broadcast_rng_state(device, src: int = 0, group=None) -> None:
+    """Rank src's RNG state (the host generator and, for a HIP device, that device's) on every
+    rank, so replicated random draws (the VAE's full-batch eps) agree without per-step traffic."""
+    if not _active(group):
+        return
+    dev = torch.device(device)
+    comm = dev if (dev.type == "cuda" and dist.get_backend(group) == "nccl") else torch.device("cpu")
+    def bcast(state):
+        buf = state.to(comm)
+        dist.broadcast(buf, src=src, group=group)
+        return buf.cpu()
+    torch.set_rng_state(bcast(torch.get_rng_state()))
+    if dev.type == "cuda":
+        torch.cuda.set_rng_state(bcast(torch.cuda.get_rng_state(dev)), dev)
+
+
 def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: torch.Tensor, group=None):
     """Global (n, mean, std, norm) from per-rank values (Chan's pooled variance, fp64)."""
     n = torch.tensor([n_local], dtype=torch.float64, device=mean.device)
@@ -96,9 +115,56 @@ def combine_stats(n_local: float, mean: torch.Tensor, std: torch.Tensor, norm: t
     return n_tot, gmean.to(mean.dtype), gstd.to(std.dtype), gnorm.to(norm.dtype)
 
 
+def combine_sums(n_local: float, sums: torch.Tensor, group=None):
+    """Global (n, mean, std, norm) from per-rank fp64 totals (sum b, sum g, sum b^2, sum g^2,
+    sum Fa^2): one differentiable 6-double all-reduce, then the kernel's own finalisation
+    (ude_stats_finalize_kernel) in fp64."""
+    n = torch.tensor([n_local], dtype=torch.float64, device=sums.device)
+    tot = all_reduce_sum(torch.cat([n, sums.double()]), group)
+    n_tot = tot[0]
+    gmean = tot[1:3] / n_tot
+    gvar = (tot[3:5] - n_tot * gmean * gmean) / (n_tot - 1.0)
+    gstd = torch.sqrt(torch.clamp(gvar, min=0.0))
+    gnorm = torch.sqrt(tot[5:6])
+    return n_tot, gmean, gstd, gnorm
+
+
+def _sync_from_sums(module, group) -> bool:
+    """The exchange on the fused solves' fp64 totals; False when some recorded entry
+    has none (eager evaluations, materialised lists, the dopri5 forward), for the fallback."""
+    from .fused import stat_sums
+    from .rhs import eager_params
+    sums = module._fused_sums
+    has_p = module.ode_type in ("Fp", "FaFp")
+    has_a = module.ode_type in ("Fa", "FaFp")
+    if not sums or eager_params(module.params):
+        return False
+    if has_p and len(module._fused_rates) != len(sums):
+        return False
+    if has_a and len(module.tracker) != len(sums):
+        return False
+    n = sum(e[0] for e in sums)
+    local = stat_sums(sums[0][1], sums[0][2], sums[0][0])
+    for e in sums[1:]:
+        local = local + stat_sums(e[1], e[2], e[0])
+    n_tot, gm, gs, gn = combine_sums(n, local, group)
+    module.params = []
+    module._fused_sums = []
+    if has_p:
+        dt = module._fused_rates[0][1].dtype
+        module._fused_rates = [(n_tot.detach(), gm.to(dt), gs.to(dt))]
+    if has_a:
+        module.tracker = [gn.to(module.tracker[0].dtype)]
+    return True
+
+
 def sync_side_stats(module, group=None) -> None:
-    """Replace the module's recorded fused-solve statistics by their global values."""
+    """Replace the module's recorded fused-solve statistics by their global values: an
+    all-reduce of the kernel's fp64 totals when every entry has them, else of the sufficient
+    statistics rebuilt from (n, mean, std, |Fa|)."""
     if not _active(group):
+        return
+    if _sync_from_sums(module, group):
         return
     # eager evaluations (params / tracker lists of per-evaluation tensors) are folded into
     # the same sufficient statistics as the fused solves' entries

@@ -63,7 +63,17 @@ def make_plan(cfg, schedule: Schedule, n_traj: int, fa_w: float, device: torch.d
     sizes = lib.query(desc, prob, dev_index)
     if sizes.act_bytes > 0 and sizes.act_bytes > act_budget(device):
         prob.recompute = 1                      # memory fallback: recompute each stage's layers
-        sizes = lib.query(desc, prob, dev_index)
+        rsizes = lib.query(desc, prob, dev_index)
+        if rsizes.act_bytes < sizes.act_bytes:
+            sizes = rsizes
+        else:
+            # no Recompute view for this model (the Bayesian GST kernels store every stage's
+            # layer inputs for the per-evaluation weight-gradient GEMM): say so, keep the store
+            import warnings
+            prob.recompute = 0
+            warnings.warn(f"{cfg}: the training store ({sizes.act_bytes / 2**30:.2f} GiB of activations) "
+                          f"exceeds the stored-activation budget ({act_budget(device) / 2**30:.2f} GiB) and "
+                          "this model has no recompute path; allocating it anyway", ResourceWarning)
     sched = torch.from_numpy(schedule.to_bytes()).to(device, non_blocking=False)
     n_eval = 4 * schedule.n_steps * n_traj * cfg[1]
     out_k = None
@@ -123,7 +133,8 @@ def sir_token_like(latent: torch.Tensor) -> torch.Tensor:
 
 
 class FusedRK4(torch.autograd.Function):
-    """Returns (latent, stats, ckpt, sir_token); ckpt (the stage inputs of every step) is only a
+    """Returns (latent, stats, ckpt, sir_token, sums); sums = the solve's fp64 totals
+    (``stat_sums`` makes them differentiable); ckpt (the stage inputs of every step) is only a
     real output when keep_ckpt is set (materialised tracking), else an empty tensor; sir_token
     (``sir_token_like``) receives compact S, I, R cotangents."""
 
@@ -153,11 +164,12 @@ class FusedRK4(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
-        ctx.mark_non_differentiable(out_ck)
-        return latent, stats, out_ck, sir_token_like(latent)
+        sums = stats_slab[:5].clone()
+        ctx.mark_non_differentiable(out_ck, sums)
+        return latent, stats, out_ck, sir_token_like(latent), sums
 
     @staticmethod
-    def backward(ctx, dlatent, dstats, _dckpt=None, dl3=None):
+    def backward(ctx, dlatent, dstats, _dckpt=None, dl3=None, _dsums=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats = ctx.saved_tensors
         dev = y0.device
@@ -194,7 +206,7 @@ class FusedRK4Dec(torch.autograd.Function):
     """Training solve with the decoder epilogue (lib/VAE.py:138, :186): the
     forward kernel emits y_hat (T, N, R) = Decoder(latent[..., :3]) and reg =
     latent_init_loss(latent[..., :3]) at the output times and writes no latent.  Returns
-    (y_hat, reg, stats, latent_token, ckpt): latent_token is a stride-0 (T, N, R, L) placeholder
+    (y_hat, reg, stats, latent_token, ckpt, sums): latent_token is a stride-0 (T, N, R, L) placeholder
     (``materialize_latent`` turns it into the real latent on demand, its cotangent flowing back
     through the token); ckpt is the training store the latent is rebuilt from.
     Backward: ude_decoder_backward (d y_hat, d reg -> the compact S, I, R cotangent, d W_dec,
@@ -229,12 +241,13 @@ class FusedRK4Dec(torch.autograd.Function):
         ctx.plan = plan
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(y0, pack, ckpt, stats, Wd)
-        ctx.mark_non_differentiable(ckpt)
+        sums = stats_slab[:5].clone()
+        ctx.mark_non_differentiable(ckpt, sums)
         token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
-        return yhat, reg[0], stats, token, ckpt
+        return yhat, reg[0], stats, token, ckpt, sums
 
     @staticmethod
-    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None):
+    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats, Wd = ctx.saved_tensors
         dev = y0.device
@@ -305,6 +318,39 @@ def materialize_latent(token: torch.Tensor, ckpt: torch.Tensor, y0: torch.Tensor
     return _LatentFromStore.apply(token, ckpt, y0.detach(), plan)
 
 
+class _StatSums(torch.autograd.Function):
+    """The fp64 totals (sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2) of one fused solve
+    (``ude_stats_finalize_kernel`` leaves them in the stats slab), differentiable through the
+    solve's ``stats`` output [mean(2), std(2), |Fa|]: the kernel backward applies, per recorded
+    rate p and A-net output a,  dmean / n + dstd (p - mean) / ((n - 1) std)  and  d|Fa| a / |Fa|;
+    the cotangent g of the sums needs  g1 + 2 g2 p  and  2 g4 a, i.e.
+      dmean = n (g1 + 2 g2 mean),  dstd = 2 g2 (n - 1) std,  d|Fa| = 2 g4 |Fa|.
+    Used by the data-parallel exchange (all-reduce the kernel's fp64 sums, no
+    re-expansion of fp32 mean / std)."""
+
+    @staticmethod
+    def forward(ctx, stats: torch.Tensor, sums: torch.Tensor, n: float):
+        ctx.save_for_backward(stats)
+        ctx.n = float(n)
+        return sums.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (stats,) = ctx.saved_tensors
+        n = ctx.n
+        st = stats.double()
+        g = g.double()
+        d = torch.zeros(5, dtype=torch.float64, device=g.device)
+        d[0:2] = n * (g[0:2] + 2.0 * g[2:4] * st[0:2])
+        d[2:4] = 2.0 * g[2:4] * (n - 1.0) * st[2:4]
+        d[4] = 2.0 * g[4] * st[4]
+        return d.to(stats.dtype), None, None
+
+
+def stat_sums(stats: torch.Tensor, sums: torch.Tensor, n: float) -> torch.Tensor:
+    return _StatSums.apply(stats, sums, n)
+
+
 def _split(flat: torch.Tensor, shapes) -> List[torch.Tensor]:
     out, off = [], 0
     for shp in shapes:
@@ -352,10 +398,12 @@ class FusedBayesRK4(torch.autograd.Function):
         ctx.plan = plan
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats, *sds)
-        return latent, stats
+        sums = stats_slab[:5].clone()
+        ctx.mark_non_differentiable(sums)
+        return latent, stats, sums
 
     @staticmethod
-    def backward(ctx, dlatent, dstats):
+    def backward(ctx, dlatent, dstats, _dsums=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats, *sds = ctx.saved_tensors
         dev = y0.device

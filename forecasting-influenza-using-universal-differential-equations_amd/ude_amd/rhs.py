@@ -114,17 +114,24 @@ class _UDEModule(nn.Module):
         self.params = []
         self.tracker = []
         self._fused_rates: List[Tuple[float, torch.Tensor, torch.Tensor]] = []
+        # (n_eval, stats, fp64 sums) of every fused solve that reported its sums (``_record_fused``)
+        self._fused_sums: List[Tuple[float, torch.Tensor, torch.Tensor]] = []
 
     def clear_tracking(self):
         """Resets the trackers (lib/models.py:148-150)."""
         self.params = []
         self.tracker = []
         self._fused_rates = []
+        self._fused_sums = []
 
     # -- fused-solver side statistics ------------------------------------------
-    def _record_fused(self, stats: torch.Tensor, n_eval: int, evals=None) -> None:
+    def _record_fused(self, stats: torch.Tensor, n_eval: int, evals=None, sums=None) -> None:
         """stats = [mean_b, mean_g, std_b, std_g, |Fa|] from one fused solve; evals = the
-        materialised (rates (E, N, R, 2), Fa (E, N, R, 3)) of its evaluations, or None."""
+        materialised (rates (E, N, R, 2), Fa (E, N, R, 3)) of its evaluations, or None; sums = the
+        solve's fp64 totals (sum b, sum g, sum b^2, sum g^2, sum Fa^2), read by the data-parallel
+        statistics exchange (distributed.sync_side_stats)."""
+        if sums is not None and evals is None:
+            self._fused_sums.append((float(n_eval), stats, sums))
         if self.ode_type in ("Fp", "FaFp"):
             self._fused_rates.append((float(n_eval), stats[0:2], stats[2:4]))
             if evals is not None:
@@ -174,6 +181,7 @@ class _UDEModule(nn.Module):
         groups.extend(self._fused_rates)
         self.params = []
         self._fused_rates = []
+        self._fused_sums = []
         if not groups:
             torch.stack([])  # same error as the reference on an empty tracker
         if len(groups) == 1:

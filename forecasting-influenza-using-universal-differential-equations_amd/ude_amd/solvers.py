@@ -146,17 +146,17 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         if func.materialize_tracking:
             raise NotImplementedError("materialize_tracking: Bayesian RHS (per-evaluation weight samples) "
                                       "is not supported")
-        latent, stats = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *(mus + sds))
-        func._record_fused(stats, plan.n_eval)
+        latent, stats, sums = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *(mus + sds))
+        func._record_fused(stats, plan.n_eval, sums=sums)
     else:
         params = []
         for lin in func.ude_linears():
             params += [lin.weight, lin.bias]
         keep = bool(func.materialize_tracking)
-        latent, stats, ckpt, sir_token = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
+        latent, stats, ckpt, sir_token, sums = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
         latent._ude_sir_token = sir_token
         evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps) if keep else None
-        func._record_fused(stats, plan.n_eval, evals)
+        func._record_fused(stats, plan.n_eval, evals, sums=sums)
     return latent
 
 

@@ -129,7 +129,10 @@ int ude_pack_weights_bayes(const UdeModelDesc* m, const UdeProblem* p, const flo
 /* Forward solve.  latent: (T, N, R, L) with T = n_out + 1.  If ckpt != NULL
  * the stage states are saved for ude_rk4_backward.  stats_out (device, 5
  * floats) receives {mean_beta, mean_gamma, std_beta, std_gamma, |Fa|}
- * (entries of an absent net are 0). */
+ * (entries of an absent net are 0); on return stats_slab[0..4] holds the fp64
+ * totals {sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2} those are
+ * formed from (the data-parallel statistics exchange all-reduces them; the
+ * same holds for ude_rk4_forward_dec and ude_dopri5_forward's workspace). */
 int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
                     const void* sched, const float* y0, float* latent, float* ckpt,
                     double* stats_slab, float* stats_out, ude_stream_t stream);

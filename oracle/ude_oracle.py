@@ -71,6 +71,10 @@ class OracleRHS:
     fa_w: float = 1.0
     params: List[torch.Tensor] = field(default_factory=list)
     tracker: List[torch.Tensor] = field(default_factory=list)
+    # test instrumentation: record every evaluation's mask decisions on the S, I, R dims
+    # ((x > 2) | (x < -1), lib/models.py:130) -- the RHS is discontinuous there
+    record_masks: bool = False
+    masks: List[torch.Tensor] = field(default_factory=list)
 
     def _mlp(self, h, ws, bs, acts):
         for w, b, act in zip(ws, bs, acts):
@@ -83,6 +87,8 @@ class OracleRHS:
         # x: (N, R, L).  Mirrors lib/models.py:230-254 (FaFp) and siblings.
         R = self.n_regions
         mask = (x > 2) | (x < -1)
+        if self.record_masks:
+            self.masks.append(mask[..., :3].detach().clone())
         flat = x.reshape(x.shape[0], -1)
         parts = []
         if self.kind in ("Fp", "FaFp"):
@@ -101,6 +107,7 @@ class OracleRHS:
     def clear_tracking(self):
         self.params = []
         self.tracker = []
+        self.masks = []
 
     def posterior(self):
         params = torch.stack(self.params).reshape(-1, 2)
@@ -232,6 +239,7 @@ class SolveResult:
     std: Optional[torch.Tensor]
     fa_norm: Optional[torch.Tensor]
     grads: Optional[dict] = None
+    masks: Optional[torch.Tensor] = None
 
 
 def solve_and_grad(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, step_size,
@@ -292,6 +300,8 @@ def _chunk_stats(args):
             out["n"], out["s1"], out["s2"] = p.shape[0], p.sum(0), p.pow(2).sum(0)
         if rhs.tracker:
             out["sf"] = float(torch.stack(rhs.tracker).double().pow(2).sum())
+        if rhs.record_masks:
+            out["masks"] = torch.stack(rhs.masks)
     rhs.clear_tracking()
     return out
 
@@ -324,9 +334,9 @@ def _chunk_grad(args):
 
 
 def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, step_size,
-                           dlatent: torch.Tensor, dmean: Optional[torch.Tensor] = None,
+                           dlatent: Optional[torch.Tensor], dmean: Optional[torch.Tensor] = None,
                            dstd: Optional[torch.Tensor] = None, dnorm: Optional[float] = None,
-                           chunk: int = 256, workers: int = 1) -> SolveResult:
+                           chunk: int = 256, workers: int = 1, masks: bool = False) -> SolveResult:
     """``solve_and_grad`` over trajectory chunks (bounded autograd memory for full-size batches),
     optionally spread over ``workers`` spawned CPU processes (small-GEMM autograd does not use
     many intra-op threads well).
@@ -338,6 +348,8 @@ def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, st
     chunk's surrogate  <lat_c, dl_c> + sum_i [dmean p_i / n + dstd (p_i - mean)^2 / (2 (n-1) std)]
     + dnorm sum_i Fa_i^2 / (2 |Fa|)  (mean, std, |Fa| held constant), whose gradient equals the
     chunk's share of the full loss gradient.  Weight gradients are summed over chunks in order.
+    masks=True also returns every evaluation's mask decisions on S, I, R: ``res.masks``
+    (E, N, R, 3) bool, evaluation order k1..k4 per step.
     """
     N = y0.shape[0]
     dt = y0.dtype
@@ -353,7 +365,9 @@ def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, st
         with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
             return list(ex.map(fn, jobs))
 
+    rhs.record_masks = masks
     st = run(_chunk_stats, [(rhs, y0[c0:c0 + chunk], t, step_size, threads) for c0 in starts])
+    rhs.record_masks = False
     latent = torch.cat([s["latent"] for s in st], 1)
     mean = std = norm = None
     n = 0
@@ -367,6 +381,10 @@ def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, st
         norm = torch.tensor(math.sqrt(sum(s["sf"] for s in st)), dtype=torch.float64)
     res = SolveResult(latent, None if mean is None else mean.to(dt), None if std is None else std.to(dt),
                       None if norm is None else norm.to(dt))
+    if masks:
+        res.masks = torch.cat([s["masks"] for s in st], 1)
+    if dlatent is None:
+        return res
     gl = run(_chunk_grad, [(rhs, y0[c0:c0 + chunk], t, step_size, dlatent[:, c0:c0 + chunk], dmean, dstd, dnorm,
                             mean, std, norm, n, threads) for c0 in starts])
     names = ["y0"]

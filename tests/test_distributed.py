@@ -18,7 +18,11 @@ from conftest import REPO, import_pkg
 WORLD = 2
 
 
-def _worker(rank, port, q):
+MODE = ["stats"]
+
+
+def _worker(rank, port, q, mode="stats"):
+    MODE[0] = mode
     try:
         sys.path.insert(0, REPO)
         import_pkg()
@@ -32,7 +36,14 @@ def _worker(rank, port, q):
         lo, hi = (0, 180) if rank == 0 else (180, 300)      # uneven shards
         p = p_all[lo:hi].clone().requires_grad_(True)
         fa = fa_all[lo:hi].clone().requires_grad_(True)
-        n_tot, m, s, nrm = udist.combine_stats(float(hi - lo), p.mean(0), p.std(0), torch.norm(fa))
+        if MODE[0] == "sums":
+            # the fused solves' path: fp64 totals made differentiable through (mean, std, |Fa|)
+            from ude_amd.fused import stat_sums
+            stats = torch.cat([p.mean(0), p.std(0), torch.norm(fa).reshape(1)])
+            raw = torch.cat([p.sum(0), (p * p).sum(0), (fa * fa).sum().reshape(1)]).detach()
+            n_tot, m, s, nrm = udist.combine_sums(float(hi - lo), stat_sums(stats, raw, float(hi - lo)))
+        else:
+            n_tot, m, s, nrm = udist.combine_stats(float(hi - lo), p.mean(0), p.std(0), torch.norm(fa))
         # every rank computes the same global loss term; grads of the SUM over ranks
         loss = (m * torch.tensor([0.3, -0.2], dtype=torch.float64)).sum() \
             + (s * torch.tensor([0.5, 0.1], dtype=torch.float64)).sum() + 0.1 * nrm.sum()
@@ -48,11 +59,12 @@ def _worker(rank, port, q):
         q.put(("err", repr(e)))
 
 
-def test_combine_stats_matches_single_process():
+@pytest.mark.parametrize("mode", ["stats", "sums"])
+def test_combine_stats_matches_single_process(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    port = 29500 + os.getpid() % 1000 + (11 if mode == "sums" else 0)
+    procs = [ctx.Process(target=_worker, args=(r, port, q, mode)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(WORLD)]
@@ -73,3 +85,21 @@ def test_combine_stats_matches_single_process():
         assert torch.allclose(rn, nrm.detach().reshape(1))
         assert torch.allclose(gp, WORLD * p_all.grad[lo:hi])
         assert torch.allclose(gf, WORLD * fa_all.grad[lo:hi])
+
+
+def test_stat_sums_cotangent_maps_onto_the_kernel_inputs(pkg):
+    """fused.stat_sums: the cotangent of the fp64 totals, handed to the kernel as (d mean, d std,
+    d |Fa|) and applied per entry as the kernel backward does, equals d/dp of the totals."""
+    from ude_amd.fused import stat_sums
+    gen = torch.Generator().manual_seed(3)
+    p = (torch.rand(50, 2, generator=gen, dtype=torch.float64) + 0.2).requires_grad_(True)
+    fa = torch.randn(50, 3, generator=gen, dtype=torch.float64).requires_grad_(True)
+    g = torch.randn(5, generator=gen, dtype=torch.float64)
+    stats = torch.cat([p.mean(0), p.std(0), torch.norm(fa).reshape(1)])
+    raw = torch.cat([p.sum(0), (p * p).sum(0), (fa * fa).sum().reshape(1)]).detach()
+    (stat_sums(stats, raw, 50.0) * g).sum().backward()
+    gp, gf = p.grad.clone(), fa.grad.clone()
+    p.grad = None
+    fa.grad = None
+    (torch.cat([p.sum(0), (p * p).sum(0), (fa * fa).sum().reshape(1)]) * g).sum().backward()
+    assert torch.allclose(gp, p.grad) and torch.allclose(gf, fa.grad)

@@ -149,3 +149,21 @@ def test_host_t_cache_tracks_inplace_updates(pkg):
     t[3] = 0.0
     with pytest.raises(AssertionError):
         solvers._host_t(t)
+
+
+def test_prebuilt_library_matches_the_tree(native):
+    """ude_build_info embeds the hash of the sources the library was compiled from; prebuilt()
+    refuses a library whose hash differs from the tree's."""
+    lib = native.prebuilt()
+    assert native.built_hash(lib) == native.source_hash()
+
+
+def test_stale_prebuilt_library_is_refused(native, monkeypatch):
+    lib = native.prebuilt()
+    monkeypatch.setattr(native, "source_hash", lambda: "0" * 16)
+    with pytest.raises(native.UdeStaleLibrary):
+        native.prebuilt()
+    native._SUPPORTED.clear()
+    with pytest.raises(native.UdeStaleLibrary):      # not silently reported as "unsupported"
+        native.config_supported(native._cfgs.PREBUILT[0])
+    native._SUPPORTED.clear()

@@ -213,7 +213,6 @@ struct Ops {
         return Ops<Recompute<M>>::forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab,
                                               stats_out, reg_out, s);
     }
-    if (M::BAYES) return UDE_E_UNSUPPORTED;
     if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !stats_out || !reg_out)
       return UDE_E_INVALID;
     if (p->n_steps < 1) return UDE_E_INVALID;

@@ -139,7 +139,7 @@ __device__ void gst_body(const GstArgs& A, float* lds) {
                               TT * M::XST_W * 4);
     const Rsrc gs = make_rsrc(A.gst + (((size_t)tile * A.n_steps + step) * 4 + jj) * TT * M::ACT_A4,
                               TT * M::ACT_A4 * 4);
-    const Rsrc ss = make_rsrc(A.ckpt + ckpt_final_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16,
+    const Rsrc ss = make_rsrc(A.ckpt + gst_static_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16,
                               TT * M::S16 * 4);
     sfor<P::NJ>([&](auto jb) {
       constexpr int j = decltype(jb)::value;

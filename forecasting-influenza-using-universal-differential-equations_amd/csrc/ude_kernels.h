@@ -472,11 +472,18 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
 
+// GST training forward: the tiles' static features ([tile][16][S16]) behind the stage checkpoints and
+// stored rows (the weight-gradient GEMM's layer-0 input beside each stage's stored input).
+template <class M>
+__host__ __device__ __forceinline__ size_t gst_static_off(int n_tiles, int n_steps) {
+  return (size_t)n_tiles * n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::XST_W : 0));
+}
 // DEC training forward: the solve's final state y_{n_steps} ([tile][F][16]) behind the stage
-// checkpoints and stored activations (the decoder backward reads every output state from there).
+// checkpoints, stored activations and (GST) static features, i.e. at ude_query's ckpt_bytes (the
+// decoder backward reads every output state from there).
 template <class M>
 __host__ __device__ __forceinline__ size_t ckpt_final_off(int n_tiles, int n_steps) {
-  return (size_t)n_tiles * n_steps * 4 * (M::F * TT + (M::ACT_STORED ? TT * M::XST_W : 0));
+  return gst_static_off<M>(n_tiles, n_steps) + (M::GST ? (size_t)n_tiles * TT * M::S16 : 0);
 }
 
 // Stored activations (Model::ACT_STORED) of one tile-stage: [16][XST_W] behind the checkpoint.
@@ -609,7 +616,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     if constexpr (TRAIN && M::GST) {
       // the tile's static features once ([tile][16][S16] behind the stored rows): the weight-gradient
       // GEMM's layer-0 input beside each stage's stored input
-      f4* dst = reinterpret_cast<f4*>(A.ckpt + ckpt_final_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16);
+      f4* dst = reinterpret_cast<f4*>(A.ckpt + gst_static_off<M>(A.n_tiles, A.n_steps) + (size_t)tile * TT * M::S16);
       constexpr int QS = M::S16 / 4;
       #pragma unroll 1
       for (int i = tid; i < TT * QS; i += NTHREADS) {

@@ -158,6 +158,32 @@ class _BayesBase(_UDEModule):
             out += [lay.w_mean + lay.z[0] * torch.abs(lay.w_std), lay.b_mean + lay.z[1] * torch.abs(lay.b_std)]
         return out
 
+    def _nets(self, x):
+        """Eager evaluation of the nets: (rates (N, R, 2) or None, Fa (N, R, 3) or None).  The layers
+        draw their own z (make_z, models_bayes.py:30-32, :43-48); with an eps stream set
+        (``set_eps_stream``) the evaluation takes its next row instead, in the layers' call order."""
+        R = self.n_regions
+        wb = self._eval_weights() if getattr(self, "_eps_next", None) is not None else None
+
+        def run(stack, h, k):
+            for m in stack:
+                if wb is not None and isinstance(m, Dense_Variational):
+                    h = nn.functional.linear(h, wb[k], wb[k + 1])
+                    k += 2
+                else:
+                    h = m(h)
+            return h, k
+
+        rates = fa = None
+        k = 0
+        if self.ode_type in ("Fp", "FaFp"):
+            h, k = run(self.Fp_net, x, k)
+            rates = torch.abs(h).reshape(-1, R, 2)
+        if self.ode_type in ("Fa", "FaFp"):
+            h, k = run(self.aug_net, x, k)
+            fa = h.reshape(-1, R, 3)
+        return rates, fa
+
     def set_eps_stream(self, eps: Optional[torch.Tensor]) -> None:
         """Use ``eps`` ((4 * n_steps, n_params)) as the draws of the next solve: the fused
         whole-solve kernel takes all of it, evaluations one at a time take a row each."""
@@ -206,7 +232,7 @@ class Bayes_Fp(_BayesBase):
         f = self._fused_forward(x)
         if f is not None:
             return f
-        rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
+        rates, _ = self._nets(x)
         self.params.append(rates)
         return _finish(_sir_flux(rates, x), x)
 
@@ -227,7 +253,7 @@ class Bayes_Fa(_BayesBase):
         f = self._fused_forward(x)
         if f is not None:
             return f
-        fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
+        _, fa = self._nets(x)
         res = _finish(fa, x)
         self.tracker.append(fa)
         return res
@@ -252,9 +278,8 @@ class Bayes_FaFp(_BayesBase):
         f = self._fused_forward(x)
         if f is not None:
             return f
-        rates = torch.abs(_run_stack(self.Fp_net, x)).reshape(-1, self.n_regions, 2)
+        rates, fa = self._nets(x)
         self.params.append(rates)
-        fa = _run_stack(self.aug_net, x).reshape(-1, self.n_regions, 3)
         res = _finish(_sir_flux(rates, x) + self.Fa_w * fa, x)
         self.tracker.append(fa)
         return res

@@ -42,7 +42,7 @@ def decoder_linear(dec) -> Optional[torch.nn.Linear]:
 def eligible(ode, y0: torch.Tensor, linear: Optional[torch.nn.Linear]) -> bool:
     from .solvers import fusable
     R = getattr(ode, "n_regions", None)
-    return (linear is not None and fusable(ode, y0) and ode.uncertainty == "none"
+    return (linear is not None and fusable(ode, y0) and ode.uncertainty in ("none", "bayes")
             and not ode.materialize_tracking and tuple(linear.weight.shape) == (R, 3 * R)
             and linear.bias is not None and linear.weight.dtype == torch.float32
             and linear.weight.device == y0.device)
@@ -73,11 +73,18 @@ def solve_decode(ode, y0: torch.Tensor, t: torch.Tensor, step_size, linear: torc
     plan = solvers.plan_for(ode, y0, t, step_size)
     if plan.out_k is None or plan.n_times > MAX_TIMES:
         return None
-    params = []
-    for lin in ode.ude_linears():
-        params += [lin.weight, lin.bias]
-    yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight,
-                                                                  linear.bias, *params)
+    if ode.uncertainty == "bayes":
+        # every evaluation's weight sample (models_bayes.py:43-48) from the solve's eps stream
+        mus, sds = ode.ude_mean_std()
+        eps = ode.take_eps(4 * plan.prob.n_steps, sum(int(p.numel()) for p in mus), y0.device)
+        yhat, reg, stats, token, ckpt, sums = _fused.FusedBayesRK4Dec.apply(
+            plan, y0.contiguous(), eps, linear.weight, linear.bias, *(mus + sds))
+    else:
+        params = []
+        for lin in ode.ude_linears():
+            params += [lin.weight, lin.bias]
+        yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight,
+                                                                      linear.bias, *params)
     ode._record_fused(stats, plan.n_eval, sums=sums)
     return yhat, reg, LazyLatent(token, ckpt, y0, plan), plan
 

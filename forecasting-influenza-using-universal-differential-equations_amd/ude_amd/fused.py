@@ -216,32 +216,14 @@ class FusedRK4Dec(torch.autograd.Function):
     def forward(ctx, plan: Plan, y0: torch.Tensor, Wd: torch.Tensor, bd: torch.Tensor, *params: torch.Tensor):
         dev = y0.device
         stream = _stream(dev)
-        sz = plan.sizes
         ws = [p.contiguous() for p in params[0::2]]
         bs = [p.contiguous() for p in params[1::2]]
-        Wd, bd = Wd.contiguous(), bd.contiguous()
-        pack = torch.empty(sz.pack_bytes // 4, dtype=torch.float32, device=dev)
+        pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
         plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
-        dec_pack = torch.empty(sz.dec_pack_bytes // 4, dtype=torch.float32, device=dev)
-        plan.lib.pack_decoder(plan.desc, Wd.data_ptr(), bd.data_ptr(), dec_pack.data_ptr(), stream)
-        N, R, L = y0.shape
-        yhat = torch.empty((plan.n_times, N, R), dtype=torch.float32, device=dev)
-        ckpt = torch.empty((sz.ckpt_bytes + sz.ckpt_final_bytes) // 4, dtype=torch.float32, device=dev)
-        stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
-        reg_slab = torch.empty(max(sz.grid_fwd, 1), dtype=torch.float64, device=dev)
-        stats = torch.zeros(5, dtype=torch.float32, device=dev)
-        reg = torch.zeros(1, dtype=torch.float32, device=dev)
-        if EVENTS is not None:
-            e0 = _ev(dev); e0.record()
-        plan.lib.forward_dec(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                             dec_pack.data_ptr(), yhat.data_ptr(), ckpt.data_ptr(), stats_slab.data_ptr(),
-                             reg_slab.data_ptr(), stats.data_ptr(), reg.data_ptr(), stream)
-        if EVENTS is not None:
-            e1 = _ev(dev); e1.record(); EVENTS.append(("fwd_dec", e0, e1))
+        yhat, reg, stats, ckpt, sums = _dec_forward(plan, y0, pack, Wd, bd)
         ctx.plan = plan
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(y0, pack, ckpt, stats, Wd)
-        sums = stats_slab[:5].clone()
+        ctx.save_for_backward(y0, pack, ckpt, stats, Wd.contiguous())
         ctx.mark_non_differentiable(ckpt, sums)
         token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
         return yhat, reg[0], stats, token, ckpt, sums
@@ -250,44 +232,115 @@ class FusedRK4Dec(torch.autograd.Function):
     def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats, Wd = ctx.saved_tensors
+        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent)
+        return (None, dy0, dWd, dbd) + tuple(_split(dparams, plan.param_shapes))
+
+
+class FusedBayesRK4Dec(torch.autograd.Function):
+    """``FusedRK4Dec`` for the Bayesian RHS (lib/in_development/models_bayes.py; run_ode.py:99
+    ``*b`` models in the VAE, lib/VAE.py:137-138): every evaluation's weight sample w_e = mean +
+    eps_e |std| packed as in ``FusedBayesRK4``, the decoder epilogue as in ``FusedRK4Dec``.
+    Inputs: plan, y0, eps, W_dec, b_dec, then the means and the raw stds (torch order)."""
+
+    @staticmethod
+    def forward(ctx, plan: Plan, y0: torch.Tensor, eps: torch.Tensor, Wd: torch.Tensor, bd: torch.Tensor,
+                *params: torch.Tensor):
         dev = y0.device
         stream = _stream(dev)
         sz = plan.sizes
-        N, R, L = y0.shape
-        T = plan.n_times
-        if dyhat is None or _is_placeholder(dyhat):
-            dyhat = torch.zeros((T, N, R), dtype=torch.float32, device=dev)
-        dyhat = dyhat.contiguous().to(torch.float32)
-        g_reg = torch.zeros(1, dtype=torch.float32, device=dev) if dreg is None else dreg.reshape(1).float()
-        dl3 = torch.empty((T, N, R, 3), dtype=torch.float32, device=dev)
-        dWd = torch.empty_like(Wd)
-        dbd = torch.empty(R, dtype=torch.float32, device=dev)
-        dec_ws = torch.empty(max(sz.dec_ws_bytes // 4, 1), dtype=torch.float32, device=dev)
-        if EVENTS is not None:
-            e0 = _ev(dev); e0.record()
-        plan.lib.decoder_backward(plan.desc, plan.prob, plan.sched_dev.data_ptr(), ckpt.data_ptr(), dyhat.data_ptr(),
-                                  Wd.data_ptr(), g_reg.data_ptr(), dec_ws.data_ptr(), dl3.data_ptr(), dWd.data_ptr(),
-                                  dbd.data_ptr(), stream)
-        if EVENTS is not None:
-            e1 = _ev(dev); e1.record(); EVENTS.append(("dec_bwd", e0, e1))
-        full = None
-        if dlatent is not None and not _is_placeholder(dlatent):
-            # the materialised latent was used too: one full cotangent
-            full = dlatent.contiguous().to(torch.float32).clone()
-            full[..., :3] += dl3
-            dl3 = None
-        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
-        dy0 = torch.empty_like(y0)
-        slab = torch.empty(max(sz.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
-        dparams = torch.empty(sz.n_params, dtype=torch.float32, device=dev)
-        if EVENTS is not None:
-            e0 = _ev(dev); e0.record()
-        plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                              ckpt.data_ptr(), _ptr(full), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
-                              dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
-        if EVENTS is not None:
-            e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
-        return (None, dy0, dWd, dbd) + tuple(_split(dparams, plan.param_shapes))
+        k = len(params) // 2
+        mus = [p.contiguous() for p in params[:k]]
+        sds = [p.contiguous() for p in params[k:]]
+        eps = eps.contiguous()
+        pack = torch.empty(max(sz.pack_bytes // 4, 1), dtype=torch.float32, device=dev)
+        plan.lib.pack_bayes(plan.desc, plan.prob, [w.data_ptr() for w in mus[0::2]], [b.data_ptr() for b in mus[1::2]],
+                            [w.data_ptr() for w in sds[0::2]], [b.data_ptr() for b in sds[1::2]], eps.data_ptr(),
+                            pack.data_ptr(), stream)
+        yhat, reg, stats, ckpt, sums = _dec_forward(plan, y0, pack, Wd, bd)
+        ctx.plan = plan
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(y0, pack, ckpt, stats, Wd.contiguous(), *sds)
+        ctx.mark_non_differentiable(ckpt, sums)
+        token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
+        return yhat, reg[0], stats, token, ckpt, sums
+
+    @staticmethod
+    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None, _dsums=None):
+        plan: Plan = ctx.plan
+        y0, pack, ckpt, stats, Wd, *sds = ctx.saved_tensors
+        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent)
+        n = plan.sizes.n_params // 2
+        d_mu = _split(dparams[:n], plan.param_shapes)
+        d_abs = _split(dparams[n:], plan.param_shapes)
+        d_sd = [g * torch.sign(s) for g, s in zip(d_abs, sds)]
+        return (None, dy0, None, dWd, dbd) + tuple(d_mu) + tuple(d_sd)
+
+
+def _dec_forward(plan: Plan, y0: torch.Tensor, pack: torch.Tensor, Wd: torch.Tensor, bd: torch.Tensor):
+    """ude_rk4_forward_dec on a packed model: (y_hat, reg, stats, training store, fp64 sums)."""
+    dev = y0.device
+    stream = _stream(dev)
+    sz = plan.sizes
+    Wd, bd = Wd.contiguous(), bd.contiguous()
+    dec_pack = torch.empty(sz.dec_pack_bytes // 4, dtype=torch.float32, device=dev)
+    plan.lib.pack_decoder(plan.desc, Wd.data_ptr(), bd.data_ptr(), dec_pack.data_ptr(), stream)
+    N, R, L = y0.shape
+    yhat = torch.empty((plan.n_times, N, R), dtype=torch.float32, device=dev)
+    ckpt = torch.empty((sz.ckpt_bytes + sz.ckpt_final_bytes) // 4, dtype=torch.float32, device=dev)
+    stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
+    reg_slab = torch.empty(max(sz.grid_fwd, 1), dtype=torch.float64, device=dev)
+    stats = torch.zeros(5, dtype=torch.float32, device=dev)
+    reg = torch.zeros(1, dtype=torch.float32, device=dev)
+    if EVENTS is not None:
+        e0 = _ev(dev); e0.record()
+    plan.lib.forward_dec(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                         dec_pack.data_ptr(), yhat.data_ptr(), ckpt.data_ptr(), stats_slab.data_ptr(),
+                         reg_slab.data_ptr(), stats.data_ptr(), reg.data_ptr(), stream)
+    if EVENTS is not None:
+        e1 = _ev(dev); e1.record(); EVENTS.append(("fwd_dec", e0, e1))
+    return yhat, reg, stats, ckpt, stats_slab[:5].clone()
+
+
+def _dec_backward(plan: Plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent):
+    """ude_decoder_backward then ude_rk4_backward_sir: (dy0, d W_dec, d b_dec, flat d params)."""
+    dev = y0.device
+    stream = _stream(dev)
+    sz = plan.sizes
+    N, R, L = y0.shape
+    T = plan.n_times
+    if dyhat is None or _is_placeholder(dyhat):
+        dyhat = torch.zeros((T, N, R), dtype=torch.float32, device=dev)
+    dyhat = dyhat.contiguous().to(torch.float32)
+    g_reg = torch.zeros(1, dtype=torch.float32, device=dev) if dreg is None else dreg.reshape(1).float()
+    dl3 = torch.empty((T, N, R, 3), dtype=torch.float32, device=dev)
+    dWd = torch.empty_like(Wd)
+    dbd = torch.empty(R, dtype=torch.float32, device=dev)
+    dec_ws = torch.empty(max(sz.dec_ws_bytes // 4, 1), dtype=torch.float32, device=dev)
+    if EVENTS is not None:
+        e0 = _ev(dev); e0.record()
+    plan.lib.decoder_backward(plan.desc, plan.prob, plan.sched_dev.data_ptr(), ckpt.data_ptr(), dyhat.data_ptr(),
+                              Wd.data_ptr(), g_reg.data_ptr(), dec_ws.data_ptr(), dl3.data_ptr(), dWd.data_ptr(),
+                              dbd.data_ptr(), stream)
+    if EVENTS is not None:
+        e1 = _ev(dev); e1.record(); EVENTS.append(("dec_bwd", e0, e1))
+    full = None
+    if dlatent is not None and not _is_placeholder(dlatent):
+        # the materialised latent was used too: one full cotangent
+        full = dlatent.contiguous().to(torch.float32).clone()
+        full[..., :3] += dl3
+        dl3 = None
+    dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+    dy0 = torch.empty_like(y0)
+    slab = torch.empty(max(sz.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
+    dparams = torch.empty(sz.n_params, dtype=torch.float32, device=dev)
+    if EVENTS is not None:
+        e0 = _ev(dev); e0.record()
+    plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                          ckpt.data_ptr(), _ptr(full), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
+                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+    if EVENTS is not None:
+        e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
+    return dy0, dWd, dbd, dparams
 
 
 class _LatentFromStore(torch.autograd.Function):

@@ -102,6 +102,8 @@ class OracleBayesRHS:
         self.n_calls += 1
         R = self.n_regions
         mask = (x > 2) | (x < -1)
+        if getattr(self, "record_masks", False):      # test instrumentation (S, I, R decisions)
+            self.masks.append(mask[..., :3].detach().clone())
         flat = x.reshape(x.shape[0], -1)
         off = 0
         if self.kind in ("Fp", "FaFp"):
@@ -122,6 +124,7 @@ class OracleBayesRHS:
     def clear_tracking(self):
         self.params = []
         self.tracker = []
+        self.masks = []
         self.n_calls = 0
 
     def posterior(self):

@@ -234,11 +234,14 @@ def make_e2e():
     print("e2e fixture written, loss", float(loss), dict(zip(names, data)))
 
 
-def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, seed):
+def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, seed, bayes=False):
     """End-to-end training step of the reference VAE at a given region count, run twice by the
     reference code itself: in fp32 (the reference's dtype) and in fp64 (the parity target; the
     fp32-vs-fp64 distance of the reference's own step sets the tolerance).  The eps draw of
-    VAE.__call__ is pinned by replacing torch.randn for the duration of the call."""
+    VAE.__call__ is pinned by replacing torch.randn for the duration of the call.  bayes: the ODE is
+    the reference's Bayes_FaFp (lib/in_development/models_bayes.py, run_ode.py:99 'UONNb'); every
+    RHS evaluation's weight draws replay the stream ``ode_eps`` through Dense_Variational.make_z
+    (tests/golden/make_golden_bayes.py inject) and the loss gains the reference's ode_kl term."""
     import copy
     import types
     td = types.ModuleType("torchdiffeq")
@@ -250,7 +253,11 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
     sys.modules["torchdiffeq"] = td
     import lib.VAE as ref_vae
     torch.manual_seed(seed)
-    model = ref_vae.VAE(ref_models.Encoder_Back_GRU, ref_models.FaFp, ref_models.Decoder, n_qs, 8, R,
+    ode_cls = ref_models.FaFp
+    if bayes:
+        import lib.in_development.models_bayes as ref_bayes
+        ode_cls = ref_bayes.Bayes_FaFp
+    model = ref_vae.VAE(ref_models.Encoder_Back_GRU, ode_cls, ref_models.Decoder, n_qs, 8, R,
                         ode_params=dict(ode_params, prior_std=0.05), enc_params=enc_params,
                         uncertainty=True, ode_kl_w=1 / 153)
     gen = torch.Generator().manual_seed(seed + 1)
@@ -265,6 +272,11 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
               "anneal": True}
     sd = {part: {k: v.clone() for k, v in getattr(model, part).state_dict().items()}
           for part in ("enc", "ode", "dec")}
+    ode_eps = None
+    if bayes:
+        n_steps = len(eval_pts) - 1                      # weekly outputs, step = t[1] - t[0]: grid = outputs
+        n_par = sum(p.numel() for p in model.ode.parameters()) // 2
+        ode_eps = torch.randn(4 * n_steps, n_par, generator=gen)
 
     def step(dtype):
         m = copy.deepcopy(model)
@@ -273,6 +285,9 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
         m.dtype = dtype
         m.enc.scaler = m.enc.scaler.to(dtype)
         m.setup_training(lr=1e-3)
+        if bayes:
+            from make_golden_bayes import inject
+            inject(m.ode, ode_eps.to(dtype))
         real_randn = torch.randn
         torch.randn = lambda *a, **k: eps.to(dtype).clone()
         try:
@@ -290,6 +305,8 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
     o32, names, data = step(torch.float32)
     o64, _, _ = step(torch.float64)
     arrs = {"x": x.numpy(), "y": y.numpy(), "t": t.numpy(), "eval_pts": eval_pts, "eps": eps.numpy()}
+    if bayes:
+        arrs["ode_eps"] = ode_eps.numpy()
     for part in ("enc", "ode", "dec"):
         for k, v in sd[part].items():
             arrs[f"w_{part}.{k}"] = v.numpy()
@@ -298,7 +315,7 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
         arrs["ref64_" + k] = v.float().numpy() if k == "latent" else v.numpy()
     arrs["ref32_loss"] = o32["loss"].numpy()
     dist = {k: normwise_rel(o32[k], o64[k]) for k in o64}
-    meta = {"B": B, "window": window, "gamma": gamma, "n_qs": n_qs, "n_regions": R, "n_samples": S_,
+    meta = {"B": B, "window": window, "gamma": gamma, "n_qs": n_qs, "n_regions": R, "n_samples": S_, "bayes": bayes,
             "losses": losses, "loss_names": names, "loss_data": data, "ode_params": ode_params,
             "enc_params": enc_params, "ref32_vs_ref64": dist,
             "generator": "tests/golden/make_golden.py make_e2e_case (reference lib/VAE.py + lib/models.py, "
@@ -328,6 +345,15 @@ def make_e2e_us():
                   seed=1111)
 
 
+def make_e2e_us_bayes():
+    # the US model as run_ode.py's 'UONNb' (Bayes_FaFp, fresh weight sample per RHS evaluation) in the
+    # VAE training step, with the reference's ode_kl term (lib/VAE.py:191-195)
+    make_e2e_case("e2e_vae_us_bayes", R=1, n_qs=90, B=8, S_=64, window=8, gamma=56,
+                  ode_params={"net_sizes": [64, 64, 32], "aug_net_sizes": [64, 64]},
+                  enc_params={"q_sizes": [32, 16], "ff_sizes": [16, 16], "SIR_scaler": [0.1, 0.05, 1.0]},
+                  seed=2222, bayes=True)
+
+
 def make_e2e_toy64():
     # the toy shapes of e2e_vae_step (S = 5, masked target), with the fp64 parity target
     make_e2e_case("e2e_vae_toy64", R=1, n_qs=3, B=4, S_=5, window=6, gamma=21,
@@ -342,6 +368,8 @@ if __name__ == "__main__":
         make_e2e_state49()
     elif len(sys.argv) > 1 and sys.argv[1] == "e2e_us":
         make_e2e_us()
+    elif len(sys.argv) > 1 and sys.argv[1] == "e2e_us_bayes":
+        make_e2e_us_bayes()
     elif len(sys.argv) > 1 and sys.argv[1] == "e2e_toy64":
         make_e2e_toy64()
     else:

@@ -35,3 +35,32 @@ def step_of(g):
 def tol(g, key, floor=1e-5):
     """max(floor, 2 x the reference's own fp32-vs-fp64 distance on this case)."""
     return max(floor, 2.0 * g["meta"]["ref32_vs_ref64"].get(key, 0.0))
+
+
+def kernel_forward_masks(pkg, mod, y0, t, step_size):
+    """The fused training forward (fp32, on mod's HIP device) of y0 with its training store kept:
+    (latent (T, N, R, L) on the host, every evaluation's mask decisions on S, I, R -- (x > 2) |
+    (x < -1) of the stage inputs the kernel evaluated, read from the store's stage-input checkpoints
+    [tile][step][stage][3R][16] -- as an (E, N, R, 3) bool host tensor, E = 4 steps)."""
+    from ude_amd import fused, solvers
+    dev = next(mod.parameters()).device
+    yd = y0.to(dev).contiguous()
+    plan = solvers.plan_for(mod, yd, t, step_size)
+    params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
+    mod.clear_tracking()
+    with torch.no_grad():
+        lat, _stats, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
+    mod.clear_tracking()
+    N, R, _L = y0.shape
+    tiles = (N + 15) // 16
+    E = 4 * plan.prob.n_steps
+    dyn = ckpt[: tiles * E * 3 * R * 16].view(tiles, E, 3 * R, 16)
+    x = dyn.permute(1, 0, 3, 2).reshape(E, tiles * 16, R, 3)[:, :N]
+    masks = ((x > 2) | (x < -1)).cpu()
+    return lat.cpu(), masks
+
+
+def agreeing_trajectories(masks_a, masks_b):
+    """(N,) bool: trajectories whose every evaluation takes the same mask decisions in a and b."""
+    E, N = masks_a.shape[:2]
+    return (masks_a == masks_b).reshape(E, N, -1).all(2).all(0)

@@ -6,15 +6,14 @@ the fp64 CPU oracle.
   365 daily RK4 steps (1,460 RHS evaluations per trajectory), forward and backward.  The oracle
   runs chunked over trajectories (exact: the side statistics enter the gradient linearly once
   their global values are known, oracle/ude_oracle.py solve_and_grad_chunked) on spawned CPU
-  workers.  Bars (written here):
-    - latent of the whole batch: <= 1e-5 normwise vs fp64 (north_star);
-    - on the trajectories that stay inside the RHS's domain [-1, 2] (see the test's docstring:
-      outside it the masked RHS is discontinuous and the gradient rounding-determined), solved
-      as a batch: latent, posterior mean / std, |Fa| <= 1e-5; every gradient <= max(2e-5, 2 x
-      the oracle's own fp32-vs-fp64 distance), the fp32 oracle run only above the 2e-5 floor.
-* BASELINE configs[1] (20,480 trajectories, R = 49): the full batch is solved on the GPU and a
-  256-row slice is checked against the fp64 oracle (latent; dy0 under a latent cotangent).
-  Slice bit-identity (test_gpu_parity.test_full_size_properties) carries this to every row.
+  workers.  The whole batch is also compared with the fp32 oracle (the reference's own
+  arithmetic).  Bars (written in each test): trajectories split by whether the kernel took the
+  fp64 oracle's mask decision ((x > 2) | (x < -1), lib/models.py:130) at every evaluation --
+  the agreeing ones' latent <= 1e-5 and dy0 <= 2e-5; the agreeing ones as a batch: posterior /
+  |Fa| <= 1e-5, every weight gradient <= max(2e-5, 2 x the fp32 oracle's own distance).
+* BASELINE configs[1] (20,480 trajectories, R = 49): the whole batch against the fp64 oracle,
+  reductions included (every dW / db, posterior mean / std, |Fa|).
+* R = 1 with more tiles than CUs (16,384 trajectories): the M3 launch of the training forward.
 * BASELINE configs[2] (dopri5 on the same batch): bit-reproducible, torchdiffeq's evaluation
   count (2 + 6 per attempt), and within the solve tolerance of the fused RK4 at a fine fixed step.
 """
@@ -23,7 +22,7 @@ import os
 import pytest
 import torch
 
-from helpers import normwise_rel
+from helpers import agreeing_trajectories, kernel_forward_masks, normwise_rel
 from oracle.ude_oracle import OracleRHS, solve_and_grad_chunked
 
 pytestmark = pytest.mark.gpu
@@ -91,24 +90,129 @@ def _scale_outputs(mod, sp, sa):
                 getattr(mod, name)[-1].bias.mul_(s)
 
 
-@pytest.mark.timeout(900)
+def _oracle(mod, y0, t, dl, dtype, stats=True, masks=True, chunk=512):
+    """The chunked oracle (oracle/ude_oracle.py solve_and_grad_chunked) in ``dtype`` on spawned
+    CPU workers: latent, posterior / |Fa|, every gradient, every evaluation's mask decisions."""
+    dm, ds, dn = (DM.to(dtype), DS.to(dtype), DN) if stats else (None, None, None)
+    return solve_and_grad_chunked(OracleRHS.from_module(mod, dtype), y0.to(dtype), t, t[1] - t[0],
+                                  None if dl is None else dl.to(dtype), dm, ds, dn, chunk=chunk,
+                                  workers=WORKERS, masks=masks)
+
+
+def _res_dict(res, names):
+    out = {"latent": res.latent, "y0": res.grads["y0"]}
+    for k in ("mean", "std", "fa_norm"):
+        if getattr(res, k) is not None:
+            out[k] = getattr(res, k)
+    for k in names:
+        out[k] = res.grads[k]
+    return out
+
+
+def _errs(a, b):
+    return {k: normwise_rel(a[k], b[k]) for k in b if k in a}
+
+
+def _fmt(d):
+    return ", ".join(f"{k} {v:.2e}" for k, v in d.items())
+
+
+STAT_KEYS = ("latent", "mean", "std", "fa_norm")
+
+
+def _assert_bars(errs, label, mod, y0, t, dl, names):
+    """latent / posterior / |Fa| <= 1e-5 (north_star); every gradient <= max(2e-5, 2 x the fp32
+    oracle's own distance to fp64), the fp32 oracle run only when a gradient is above the floor."""
+    for k in STAT_KEYS:
+        if k in errs:
+            assert errs[k] <= 1e-5, f"{label} {k}: {errs[k]:.3e} > 1e-5"
+    over = [k for k, v in errs.items() if k not in STAT_KEYS and v > 2e-5]
+    if over:
+        o64 = _res_dict(_oracle(mod, y0, t, dl, torch.float64, masks=False), names)
+        o32 = _res_dict(_oracle(mod, y0, t, dl, torch.float32, masks=False), names)
+        for k in over:
+            bar = 2.0 * normwise_rel(o32[k], o64[k])
+            print(f"  {label} {k}: {errs[k]:.2e} vs the fp32 oracle's own {bar / 2:.2e}")
+            assert errs[k] <= bar, f"{label} {k}: {errs[k]:.3e} > max(2e-5, {bar:.3e})"
+
+
+def _full_batch(pkg, mod, y0, t, dl, label, fp32_whole=False):
+    """Whole batch on the GPU (training forward with its store kept, for the kernel's own mask
+    decisions; then forward + VJP with the posterior / |Fa| terms) against the fp64 oracle over the
+    same batch.  Trajectories are split by whether the kernel took the fp64 oracle's mask decision
+    ((x > 2) | (x < -1) on S, I, R, lib/models.py:130 -- a discontinuity of the RHS) at every one of
+    their evaluations.  fp32_whole: also the fp32 oracle (the reference's own arithmetic) over the
+    whole batch, and the kernel's distance to it."""
+    h = t[1] - t[0]
+    N = y0.shape[0]
+    mg = mod.to(DEV)
+    lat_k, mk = kernel_forward_masks(pkg, mg, y0, t, h)
+    got, names = _gpu_vjp(pkg, mod, y0, t, dl)
+    assert torch.equal(got["latent"], lat_k)          # the same training forward, bit for bit
+    r64 = _oracle(mod, y0, t, dl, torch.float64)
+    ref = _res_dict(r64, names)
+    agree = agreeing_trajectories(mk, r64.masks)
+    K = int(agree.sum())
+    ever = int(r64.masks.reshape(r64.masks.shape[0], N, -1).any(2).any(0).sum())
+    whole = _errs(got, ref)
+    lines = [f"{label}: {K}/{N} trajectories take the fp64 oracle's mask decision at every evaluation "
+             f"({ever} are masked at some evaluation)",
+             "  whole batch, kernel vs fp64: " + _fmt(whole)]
+    r32 = None
+    if fp32_whole:
+        r32 = _oracle(mod, y0, t, dl, torch.float32)
+        o32 = _res_dict(r32, names)
+        agree32 = agreeing_trajectories(r32.masks, r64.masks)
+        k32 = int(agree32.sum())
+        lines.append(f"  fp32 oracle: {k32}/{N} trajectories agree with fp64; the kernel and the fp32 "
+                     f"oracle decide alike on {int(agreeing_trajectories(mk, r32.masks).sum())}")
+        lines.append("  whole batch, fp32 oracle vs fp64: " + _fmt(_errs(o32, ref)))
+        lines.append("  whole batch, kernel vs fp32 oracle: " + _fmt(_errs(got, o32)))
+        if k32:
+            lines.append(f"  fp32 oracle on its {k32} agreeing trajectories: latent "
+                         f"{normwise_rel(r32.latent[:, agree32], r64.latent[:, agree32]):.2e}, y0 "
+                         f"{normwise_rel(r32.grads['y0'][agree32], r64.grads['y0'][agree32]):.2e}")
+    split = {}
+    if K:
+        split["latent"] = normwise_rel(got["latent"][:, agree], r64.latent[:, agree])
+        split["y0"] = normwise_rel(got["y0"][agree], r64.grads["y0"][agree])
+    diff = (got["y0"].double() - r64.grads["y0"].double()).reshape(N, -1).pow(2).sum(1)
+    share = float(diff[~agree].sum() / diff.sum()) if float(diff.sum()) > 0 else 0.0
+    lines.append(f"  kernel on its {K} agreeing trajectories: " + _fmt(split) +
+                 f"; the {N - K} disagreeing ones carry {100 * share:.1f}% of the whole-batch dy0 error^2")
+    print("\n".join(lines))
+    return got, ref, r32, agree, names, whole, split
+
+
+def _agreeing_batch(pkg, mod, y0, t, dl, agree, names, label):
+    """The agreeing trajectories solved as a batch of their own: posterior / |Fa| and every weight
+    gradient against the fp64 oracle over the same trajectories."""
+    yk, dk = y0[agree].contiguous(), dl[:, agree].contiguous()
+    gk, _ = _gpu_vjp(pkg, mod, yk, t, dk)
+    rk = _res_dict(_oracle(mod, yk, t, dk, torch.float64, masks=False), names)
+    errs = _errs(gk, rk)
+    print(f"  the {int(agree.sum())} agreeing trajectories as one batch: " + _fmt(errs))
+    _assert_bars(errs, label, mod, yk, t, dk, names)
+
+
+@pytest.mark.timeout(1500)
 @pytest.mark.parametrize("kind,net,aug,sa", [("FaFp", [64, 64, 32], [64, 64], 1.0),
                                              ("FaFp", [64, 64, 32], [64, 64], 0.01),
                                              ("Fp", [32, 32], None, 1.0)],
                          ids=["FaFp_64_64_32", "FaFp_64_64_32_Fa_x0.01", "Fp_32_32"])
 def test_north_star_m1_full_size(pkg, kind, net, aug, sa):
-    """Forward: every trajectory of the 4096 x 365-step batch within 1e-5 of fp64 (north_star).
+    """M1 (4096 x 365 daily steps, 1,460 evaluations per trajectory), whole batch, forward + VJP,
+    against the fp64 oracle and against the fp32 oracle (the reference's own arithmetic).
 
-    VJP: the RHS is masked to zero outside [-1, 2] (lib/models.py:130) -- a discontinuity.  With
-    the default init 99.5% of the FaFp trajectories leave that domain within the year
-    (tools/ns_cond.py); an evaluation next to the boundary is masked or not by rounding, so such a
-    trajectory's gradient is itself rounding-determined (the fp32 oracle's per-trajectory dy0
-    errors reach 9e-4 there, 1.7e-4 / 2e-5 batch-wide for the kernel / the fp32 oracle).  The
-    gradient bars therefore apply to the trajectories that stay inside the domain, solved as a
-    batch of their own (their solutions are bit-identical to the full batch's rows): y0, posterior /
-    |Fa| terms and every weight gradient.  The Fa x 0.01 variant (trained-model magnitudes of the
-    augmentation) keeps ~90% of the batch in the domain."""
-    from oracle.ude_oracle import odeint_rk4
+    The RHS is masked to zero outside [-1, 2] (lib/models.py:130): with the default init nearly
+    every FaFp trajectory crosses that boundary within the year, and a trajectory whose evaluation
+    lands next to it is masked or not by rounding -- its gradient then follows another branch of a
+    discontinuous map.  Bars: every trajectory whose evaluations all take the fp64
+    oracle's mask decisions -- latent <= 1e-5, dy0 <= 2e-5 (normwise over those rows of the
+    whole-batch solve); those trajectories solved as a batch of their own -- posterior / |Fa| <=
+    1e-5, every weight gradient <= max(2e-5, 2 x the fp32 oracle's own distance); the whole batch's
+    latent <= 1e-5, or <= 2 x the fp32 oracle's own distance.  The counts, the fp32 oracle's own
+    numbers and the disagreeing trajectories' share of the whole-batch dy0 error are printed."""
     torch.manual_seed(0)
     kw = {"net_sizes": net} if net else {}
     if aug:
@@ -119,71 +223,62 @@ def test_north_star_m1_full_size(pkg, kind, net, aug, sa):
     y0, gen = _y0(N, 1, 8, 11)
     t = torch.arange(n_t, dtype=torch.float32) / 7.0
     dl = torch.randn((n_t, N, 1, 8), generator=gen, dtype=torch.float64)
-    # forward, whole batch
-    mg = mod.to(DEV)
-    mg.clear_tracking()
-    with torch.no_grad():
-        lat = pkg.odeint(mg, y0.to(DEV), t, method="rk4", options=dict(step_size=t[1] - t[0])).cpu()
-    mod.cpu()
-    with torch.no_grad():
-        rhs = OracleRHS.from_module(mod, torch.float64)
-        lat64 = odeint_rk4(rhs, y0.double(), t, t[1] - t[0])
-        rhs.clear_tracking()
-    e_lat = normwise_rel(lat, lat64)
-    sir = lat64[..., :3]
-    inside = ((sir > -1) & (sir < 2)).flatten(1).all(0).reshape(N, -1).all(1)
-    K = int(inside.sum())
-    print(f"north-star {kind} (Fa x{sa}): latent {e_lat:.2e} on all {N}; {K}/{N} trajectories stay in [-1, 2]")
-    if e_lat > 1e-5:
-        # trajectories that cross the mask boundary do so at a rounding-determined stage: the whole
-        # batch is held to the fp32 oracle's own distance, the in-domain ones (below) to 1e-5
-        with torch.no_grad():
-            r32 = OracleRHS.from_module(mod, torch.float32)
-            lat32 = odeint_rk4(r32, y0, t, t[1] - t[0])
-        bar = 2.0 * normwise_rel(lat32, lat64)
-        print(f"  whole-batch latent bar: 2 x the fp32 oracle's {bar / 2:.2e}")
-        assert e_lat <= bar
-    assert K >= 16, "too few in-domain trajectories for the gradient check"
-    # VJP on the in-domain trajectories
-    yk, dk = y0[inside].contiguous(), dl[:, inside].contiguous()
-    got, names = _gpu_vjp(pkg, mod, yk, t, dk)
-    ref = solve_and_grad_chunked(OracleRHS.from_module(mod, torch.float64), yk.double(), t, t[1] - t[0], dk,
-                                 DM, DS, DN, chunk=256, workers=WORKERS)
-    errs = {"latent": normwise_rel(got["latent"], ref.latent)}
-    if "mean" in got:
-        errs["mean"], errs["std"] = normwise_rel(got["mean"], ref.mean), normwise_rel(got["std"], ref.std)
-    if "fa_norm" in got:
-        errs["fa_norm"] = normwise_rel(got["fa_norm"], ref.fa_norm)
-    gerr = {k: normwise_rel(got[k], ref.grads[k]) for k in ["y0"] + names}
-    print(f"  VJP on {K} trajectories: " + ", ".join(f"{k} {v:.2e}" for k, v in {**errs, **gerr}.items()))
-    for k, v in errs.items():
-        assert v <= 1e-5, f"{k}: {v:.3e} > 1e-5"
-    over = [k for k, v in gerr.items() if v > 2e-5]
-    if over:
-        # the bar is max(2e-5, 2 x the oracle's own fp32 distance) for the gradients
-        r32 = solve_and_grad_chunked(OracleRHS.from_module(mod, torch.float32), yk, t, t[1] - t[0], dk.float(),
-                                     DM.float(), DS.float(), DN, chunk=256, workers=WORKERS)
-        for k in over:
-            bar = 2.0 * normwise_rel(r32.grads[k], ref.grads[k])
-            assert gerr[k] <= bar, f"{k}: {gerr[k]:.3e} > max(2e-5, {bar:.3e})"
+    label = f"north-star {kind} (Fa x{sa})"
+    got, ref, r32, agree, names, whole, split = _full_batch(pkg, mod, y0, t, dl, label, fp32_whole=True)
+    if whole["latent"] > 1e-5:
+        bar = 2.0 * normwise_rel(r32.latent, ref["latent"])
+        assert whole["latent"] <= bar, f"whole-batch latent {whole['latent']:.3e} > 2 x the fp32 oracle's {bar / 2:.3e}"
+    assert int(agree.sum()) >= 16, "too few agreeing trajectories for the gradient check"
+    assert split["latent"] <= 1e-5, split
+    assert split["y0"] <= 2e-5, split
+    _agreeing_batch(pkg, mod, y0, t, dl, agree, names, label)
 
 
-@pytest.mark.timeout(600)
-def test_state49_full_batch_slice_vs_oracle(pkg):
+@pytest.mark.timeout(1800)
+def test_state49_full_batch_vs_oracle(pkg):
+    """BASELINE configs[1] at full size: 20,480 trajectories x R = 49, 8 weekly steps, forward + VJP
+    with the posterior / |Fa| terms, the WHOLE batch against the fp64 oracle (chunked on CPU
+    workers): latent, posterior mean / std, |Fa| <= 1e-5; dy0 and every dW / db -- the 1,280-tile
+    fixed-order slab reduction + ude_grad_finalize -- <= max(2e-5, 2 x the fp32 oracle's own
+    distance).  If some trajectory's mask decisions differed from fp64 the bars would move to the
+    agreeing trajectories (the count is printed)."""
     torch.manual_seed(0)
     mod = pkg.FaFp(49, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
-    N, K = 20480, 256
+    N = 20480
     y0, gen = _y0(N, 49, 8, 5)
     t = torch.arange(9, dtype=torch.float32)
     dl = torch.randn((9, N, 49, 8), generator=gen, dtype=torch.float64)
-    got, _ = _gpu_vjp(pkg, mod, y0, t, dl, stats=False)
-    rows = torch.arange(N // 2 - K // 2, N // 2 + K // 2)      # a slice from the middle of the batch
-    ref = solve_and_grad_chunked(OracleRHS.from_module(mod, torch.float64), y0[rows].double(), t, t[1] - t[0],
-                                 dl[:, rows], chunk=32, workers=min(WORKERS, 8))
-    e_lat = normwise_rel(got["latent"][:, rows], ref.latent)
-    e_dy0 = normwise_rel(got["y0"][rows], ref.grads["y0"])
-    print(f"state49 slice: latent {e_lat:.2e}, dy0 {e_dy0:.2e}")
-    assert e_lat <= 1e-5 and e_dy0 <= 2e-5
+    got, ref, _, agree, names, whole, split = _full_batch(pkg, mod, y0, t, dl, "state49 full batch")
+    if int(agree.sum()) == N:
+        _assert_bars(whole, "state49", mod, y0, t, dl, names)
+    else:
+        assert split["latent"] <= 1e-5 and split["y0"] <= 2e-5, split
+        _agreeing_batch(pkg, mod, y0, t, dl, agree, names, "state49 agreeing")
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("kind,net,aug", [("FaFp", [64, 64, 32], [64, 64]), ("Fp", [32, 32], None)],
+                         ids=["FaFp_64_64_32", "Fp_32_32"])
+def test_r1_more_tiles_than_cus_full_batch(pkg, kind, net, aug):
+    """R = 1 with more tiles than CUs (16,384 trajectories = 1,024 tiles): the 4-wave training forward
+    at two workgroups per CU (ude_entry.h, the M3 launch) instead of the one-tile-per-CU split
+    forward the smaller R = 1 tests take.  Whole batch, 8 weekly steps, against the fp64 oracle:
+    latent / posterior / |Fa| <= 1e-5, dy0 and every weight gradient <= max(2e-5, 2 x fp32 oracle)."""
+    torch.manual_seed(1)
+    kw = {"net_sizes": net}
+    if aug:
+        kw["aug_net_sizes"] = aug
+    mod = getattr(pkg, kind)(1, latent_dim=8, **kw)
+    N = 16384
+    y0, gen = _y0(N, 1, 8, 13)
+    t = torch.arange(9, dtype=torch.float32)
+    dl = torch.randn((9, N, 1, 8), generator=gen, dtype=torch.float64)
+    got, ref, _, agree, names, whole, split = _full_batch(pkg, mod, y0, t, dl, f"R=1 {kind} N={N}")
+    if int(agree.sum()) == N:
+        _assert_bars(whole, f"R=1 {kind}", mod, y0, t, dl, names)
+    else:
+        assert split["latent"] <= 1e-5 and split["y0"] <= 2e-5, split
+        _agreeing_batch(pkg, mod, y0, t, dl, agree, names, f"R=1 {kind} agreeing")
 
 
 @pytest.mark.timeout(600)

@@ -184,6 +184,52 @@ class _BayesBase(_UDEModule):
             fa = h.reshape(-1, R, 3)
         return rates, fa
 
+    @torch.no_grad()
+    def _evals_from_checkpoint(self, ckpt: torch.Tensor, y0: torch.Tensor, n_steps: int, eps: torch.Tensor = None):
+        """``materialize_tracking`` for the Bayesian RHS: every evaluation's rates / A-net output,
+        recomputed from the stage inputs the training forward checkpoints and evaluation e's own
+        weight sample w_e = mean + eps[e] |std| (the row the whole-solve kernel used)."""
+        N, R, L = y0.shape
+        tiles = (N + 15) // 16
+        E = 4 * n_steps
+        dyn = ckpt[: tiles * n_steps * 4 * 3 * R * 16].view(tiles, E, 3 * R, 16)
+        static = y0.detach()[..., 3:]
+        mus, sds = self.ude_mean_std()
+        mu = torch.cat([p.detach().reshape(-1) for p in mus])
+        sd = torch.cat([p.detach().reshape(-1).abs() for p in sds])
+        shapes = [p.shape for p in mus]
+        rates = torch.empty((E, N, R, 2), dtype=y0.dtype, device=y0.device) if self.ode_type != "Fa" else None
+        fas = torch.empty((E, N, R, 3), dtype=y0.dtype, device=y0.device) if self.ode_type != "Fp" else None
+
+        def run(stack, h, wb, k):
+            for m in stack:
+                if isinstance(m, Dense_Variational):
+                    h = nn.functional.linear(h, wb[k], wb[k + 1])
+                    k += 2
+                else:
+                    h = m(h)
+            return h, k
+
+        for e in range(E):
+            flat = mu + eps[e].to(mu) * sd
+            wb, off = [], 0
+            for shp in shapes:
+                n = 1
+                for v in shp:
+                    n *= v
+                wb.append(flat[off:off + n].view(shp))
+                off += n
+            d = dyn[:, e].permute(0, 2, 1).reshape(tiles * 16, R, 3)[:N]
+            x = torch.cat([d, static], -1)
+            k = 0
+            if rates is not None:
+                h, k = run(self.Fp_net, x, wb, k)
+                rates[e] = torch.abs(h).reshape(N, R, 2)
+            if fas is not None:
+                h, k = run(self.aug_net, x, wb, k)
+                fas[e] = h.reshape(N, R, 3)
+        return rates, fas
+
     def set_eps_stream(self, eps: Optional[torch.Tensor]) -> None:
         """Use ``eps`` ((4 * n_steps, n_params)) as the draws of the next solve: the fused
         whole-solve kernel takes all of it, evaluations one at a time take a row each."""

@@ -420,12 +420,13 @@ class FusedBayesRK4(torch.autograd.Function):
     solve uses its own weight sample w_e = mean + eps_e * |std| (Dense_Variational
     .forward, :43-48), eps = the (4 n_steps, n_params) draw stream.
 
-    Inputs: plan, y0, eps, then the means (w, b per layer, torch order) and the raw
+    Inputs: plan, y0, eps, keep_ckpt, then the means (w, b per layer, torch order) and the raw
     stds in the same order.  The kernel returns d/d mean and d/d |std|; the sign of
-    std (torch's abs backward) is applied here."""
+    std (torch's abs backward) is applied here.  Returns (latent, stats, ckpt, sums): ckpt is the
+    training store when keep_ckpt is set (materialised tracking), else an empty tensor."""
 
     @staticmethod
-    def forward(ctx, plan: Plan, y0: torch.Tensor, eps: torch.Tensor, *params: torch.Tensor):
+    def forward(ctx, plan: Plan, y0: torch.Tensor, eps: torch.Tensor, keep_ckpt: bool, *params: torch.Tensor):
         dev = y0.device
         stream = _stream(dev)
         sz = plan.sizes
@@ -439,7 +440,8 @@ class FusedBayesRK4(torch.autograd.Function):
                             pack.data_ptr(), stream)
         latent = torch.empty((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         need_grad = any(ctx.needs_input_grad[1:])
-        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) if need_grad else None
+        ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
+            if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
         stats = torch.zeros(5, dtype=torch.float32, device=dev)
         if EVENTS is not None:
@@ -452,11 +454,12 @@ class FusedBayesRK4(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats, *sds)
         sums = stats_slab[:5].clone()
-        ctx.mark_non_differentiable(sums)
-        return latent, stats, sums
+        out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
+        ctx.mark_non_differentiable(out_ck, sums)
+        return latent, stats, out_ck, sums
 
     @staticmethod
-    def backward(ctx, dlatent, dstats, _dsums=None):
+    def backward(ctx, dlatent, dstats, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
         y0, pack, ckpt, stats, *sds = ctx.saved_tensors
         dev = y0.device
@@ -479,4 +482,4 @@ class FusedBayesRK4(torch.autograd.Function):
         d_mu = _split(dparams[:n], plan.param_shapes)
         d_abs = _split(dparams[n:], plan.param_shapes)
         d_sd = [g * torch.sign(s) for g, s in zip(d_abs, sds)]
-        return (None, dy0, None) + tuple(d_mu) + tuple(d_sd)
+        return (None, dy0, None, None) + tuple(d_mu) + tuple(d_sd)

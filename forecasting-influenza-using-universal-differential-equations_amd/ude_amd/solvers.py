@@ -143,11 +143,10 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         mus, sds = func.ude_mean_std()
         n_par = sum(int(p.numel()) for p in mus)
         eps = func.take_eps(4 * plan.prob.n_steps, n_par, y0.device)
-        if func.materialize_tracking:
-            raise NotImplementedError("materialize_tracking: Bayesian RHS (per-evaluation weight samples) "
-                                      "is not supported")
-        latent, stats, sums = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, *(mus + sds))
-        func._record_fused(stats, plan.n_eval, sums=sums)
+        keep = bool(func.materialize_tracking)
+        latent, stats, ckpt, sums = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, keep, *(mus + sds))
+        evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps, eps) if keep else None
+        func._record_fused(stats, plan.n_eval, evals, sums=sums)
     else:
         params = []
         for lin in func.ude_linears():

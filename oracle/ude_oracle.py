@@ -75,6 +75,7 @@ class OracleRHS:
     # ((x > 2) | (x < -1), lib/models.py:130) -- the RHS is discontinuous there
     record_masks: bool = False
     masks: List[torch.Tensor] = field(default_factory=list)
+    margins: List[torch.Tensor] = field(default_factory=list)     # per evaluation: (N,) distance to the boundary
 
     def _mlp(self, h, ws, bs, acts):
         for w, b, act in zip(ws, bs, acts):
@@ -89,6 +90,8 @@ class OracleRHS:
         mask = (x > 2) | (x < -1)
         if self.record_masks:
             self.masks.append(mask[..., :3].detach().clone())
+            xs = x[..., :3].detach()
+            self.margins.append(torch.minimum((xs - 2).abs(), (xs + 1).abs()).reshape(x.shape[0], -1).amin(1))
         flat = x.reshape(x.shape[0], -1)
         parts = []
         if self.kind in ("Fp", "FaFp"):
@@ -108,6 +111,7 @@ class OracleRHS:
         self.params = []
         self.tracker = []
         self.masks = []
+        self.margins = []
 
     def posterior(self):
         params = torch.stack(self.params).reshape(-1, 2)
@@ -240,6 +244,7 @@ class SolveResult:
     fa_norm: Optional[torch.Tensor]
     grads: Optional[dict] = None
     masks: Optional[torch.Tensor] = None
+    margin: Optional[torch.Tensor] = None      # (N,) min distance of S, I, R to the mask boundary
 
 
 def solve_and_grad(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, step_size,
@@ -302,6 +307,7 @@ def _chunk_stats(args):
             out["sf"] = float(torch.stack(rhs.tracker).double().pow(2).sum())
         if rhs.record_masks:
             out["masks"] = torch.stack(rhs.masks)
+            out["margin"] = torch.stack(rhs.margins).amin(0)
     rhs.clear_tracking()
     return out
 
@@ -383,6 +389,7 @@ def solve_and_grad_chunked(rhs: OracleRHS, y0: torch.Tensor, t: torch.Tensor, st
                       None if norm is None else norm.to(dt))
     if masks:
         res.masks = torch.cat([s["masks"] for s in st], 1)
+        res.margin = torch.cat([s["margin"] for s in st], 0)
     if dlatent is None:
         return res
     gl = run(_chunk_grad, [(rhs, y0[c0:c0 + chunk], t, step_size, dlatent[:, c0:c0 + chunk], dmean, dstd, dnorm,

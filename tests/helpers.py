@@ -37,7 +37,7 @@ def tol(g, key, floor=1e-5):
     return max(floor, 2.0 * g["meta"]["ref32_vs_ref64"].get(key, 0.0))
 
 
-def kernel_forward_masks(pkg, mod, y0, t, step_size):
+def kernel_forward_masks(pkg, mod, y0, t, step_size, eps=None):
     """The fused training forward (fp32, on mod's HIP device) of y0 with its training store kept:
     (latent (T, N, R, L) on the host, every evaluation's mask decisions on S, I, R -- (x > 2) |
     (x < -1) of the stage inputs the kernel evaluated, read from the store's stage-input checkpoints
@@ -46,10 +46,14 @@ def kernel_forward_masks(pkg, mod, y0, t, step_size):
     dev = next(mod.parameters()).device
     yd = y0.to(dev).contiguous()
     plan = solvers.plan_for(mod, yd, t, step_size)
-    params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
     mod.clear_tracking()
     with torch.no_grad():
-        lat, _stats, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
+        if mod.uncertainty == "bayes":          # eps: the solve's (4 n_steps, n_params) draw stream
+            mus, sds = mod.ude_mean_std()
+            lat, _stats, ckpt, _sums = fused.FusedBayesRK4.apply(plan, yd, eps.to(dev), True, *(mus + sds))
+        else:
+            params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
+            lat, _stats, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
     mod.clear_tracking()
     N, R, _L = y0.shape
     tiles = (N + 15) // 16
@@ -64,3 +68,21 @@ def agreeing_trajectories(masks_a, masks_b):
     """(N,) bool: trajectories whose every evaluation takes the same mask decisions in a and b."""
     E, N = masks_a.shape[:2]
     return (masks_a == masks_b).reshape(E, N, -1).all(2).all(0)
+
+
+class EvalMaskRecorder:
+    """Records every evaluation's mask decisions on S, I, R of a module called one evaluation at a
+    time (a forward pre-hook): ``masks`` (E, N, R, 3) bool on the host after ``close``."""
+
+    def __init__(self, mod):
+        self._m = []
+        self._h = mod.register_forward_pre_hook(self._hook)
+
+    def _hook(self, mod, args):
+        x = args[1].detach()[..., :3]
+        self._m.append(((x > 2) | (x < -1)).cpu())
+
+    def close(self):
+        self._h.remove()
+        self.masks = torch.stack(self._m)
+        return self.masks

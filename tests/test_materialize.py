@@ -102,3 +102,42 @@ def test_materialized_then_eager_evaluation_pooled(pkg):
         posts.append(m.posterior())
     assert normwise_rel(posts[0].loc, posts[1].loc) < 1e-5
     assert normwise_rel(posts[0].scale, posts[1].scale) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 10])
+def test_materialized_lists_bayes(pkg, R):
+    """Bayesian RHS (lib/in_development/models_bayes.py: every evaluation its own weight sample):
+    the materialised per-evaluation rates / A-net outputs rebuilt from the training store and each
+    evaluation's eps row equal the eager host solve on the same draws (eps stream replayed), and the
+    gradients equal the statistics-only fused solve's.  R = 10 is a GST (per-evaluation GEMM) model."""
+    import ude_amd.bayes as B
+    torch.manual_seed(13)
+    mod = B.Bayes_FaFp(R, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+    gen = torch.Generator().manual_seed(14)
+    with torch.no_grad():
+        for p in mod.ude_mean_std()[1]:
+            p.copy_(0.05 * torch.randn(p.shape, generator=gen))
+    N = 37
+    S = torch.rand(N, R, generator=gen) * 0.4 + 0.5
+    I = torch.rand(N, R, generator=gen) * 0.05
+    y0 = torch.cat([S[..., None], I[..., None], (1 - S - I)[..., None], 0.3 * torch.randn(N, R, 5, generator=gen)], -1)
+    t = torch.arange(5, dtype=torch.float32)
+    n_par = sum(p.numel() for p in mod.ude_mean_std()[0])
+    eps = torch.randn(4 * (len(t) - 1), n_par, generator=gen)
+    mod_c = B.Bayes_FaFp(R, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+    mod_c.load_state_dict(mod.state_dict())
+    mod = mod.to("cuda")
+    out = []
+    for m, dev, mat in ((mod, "cuda", True), (mod_c, "cpu", False), (mod, "cuda", False)):
+        m.set_eps_stream(eps.to(dev))
+        out.append(_solve(pkg, m, y0.to(dev).requires_grad_(True), t, mat))
+    (p_f, tr_f, post_f, nrm_f, g_f), (p_e, tr_e, post_e, nrm_e, g_e), (_, _, _, _, g_s) = out
+    assert len(p_f) == len(p_e) == 4 * (len(t) - 1) == len(tr_f) == len(tr_e)
+    for a, b in zip(p_f + tr_f, p_e + tr_e):
+        assert a.shape == b.shape and normwise_rel(a, b) < 1e-5
+    assert normwise_rel(post_f.loc, post_e.loc) < 1e-5 and normwise_rel(post_f.scale, post_e.scale) < 1e-5
+    assert normwise_rel(nrm_f, nrm_e) < 1e-5
+    for k in g_e:
+        assert normwise_rel(g_f[k], g_e[k]) < 5e-5, (k, normwise_rel(g_f[k], g_e[k]))
+        assert normwise_rel(g_f[k], g_s[k]) < 1e-5, k

@@ -518,6 +518,8 @@ def main():
     ap.add_argument("--workload", default="state49", choices=sorted(WORKLOADS))
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: every rank solves the workload's batch; strong: the batch is split over ranks")
+    ap.add_argument("--n-traj", type=int, default=None,
+                    help="development: override the workload's trajectory count (not a benchmark line)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--lines", default=None, help="comma-separated subset of the extra lines (development)")
@@ -560,6 +562,8 @@ def main():
     from ude_amd import distributed as udist
 
     w = WORKLOADS[args.workload]
+    if args.n_traj:
+        w = dict(w, n_traj=args.n_traj, desc=w["desc"] + f" [n_traj overridden: {args.n_traj}]")
     per_rank = w["n_traj"] if args.scaling == "weak" else w["n_traj"] // world
     if args.scaling == "strong" and per_rank * world != w["n_traj"]:
         raise SystemExit(f"strong scaling: {w['n_traj']} trajectories do not split over {world} ranks")

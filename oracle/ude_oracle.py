@@ -76,10 +76,22 @@ class OracleRHS:
     record_masks: bool = False
     masks: List[torch.Tensor] = field(default_factory=list)
     margins: List[torch.Tensor] = field(default_factory=list)     # per evaluation: (N,) distance to the boundary
+    # test instrumentation: "rev4" sums every Linear's K products in blocks of 4, last block first --
+    # the same fp32 arithmetic with another summation order (a second sample of fp32 rounding)
+    k_order: str = "torch"
+
+    def _linear(self, h, w, b):
+        if self.k_order != "rev4":
+            return torch.nn.functional.linear(h, w, b)
+        K = h.shape[-1]
+        acc = b.expand(h.shape[:-1] + (w.shape[0],))
+        for k0 in reversed(range(0, K, 4)):
+            acc = acc + h[..., k0:k0 + 4] @ w[:, k0:k0 + 4].T
+        return acc
 
     def _mlp(self, h, ws, bs, acts):
         for w, b, act in zip(ws, bs, acts):
-            h = torch.nn.functional.linear(h, w, b)
+            h = self._linear(h, w, b)
             if act:
                 h = torch.nn.functional.elu(h)
         return h

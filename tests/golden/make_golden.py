@@ -304,6 +304,26 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
 
     o32, names, data = step(torch.float32)
     o64, _, _ = step(torch.float64)
+    dist_b = None
+    if bayes:
+        # a second fp32 run of the same reference step with every Linear's products summed in another
+        # order (blocks of 4 along K, last block first): a second sample of fp32 rounding for the
+        # ill-conditioned terms (the decoder gradients through nll_loss's per-window sample std)
+        lin = torch.nn.functional.linear
+
+        def rev4(h, w, b=None):
+            K = h.shape[-1]
+            acc = None if b is None else b.expand(h.shape[:-1] + (w.shape[0],))
+            for k0 in reversed(range(0, K, 4)):
+                part = h[..., k0:k0 + 4] @ w[:, k0:k0 + 4].T
+                acc = part if acc is None else acc + part
+            return acc
+        torch.nn.functional.linear = rev4
+        try:
+            o32b, _, _ = step(torch.float32)
+        finally:
+            torch.nn.functional.linear = lin
+        dist_b = {k: normwise_rel(o32b[k], o64[k]) for k in o64}
     arrs = {"x": x.numpy(), "y": y.numpy(), "t": t.numpy(), "eval_pts": eval_pts, "eps": eps.numpy()}
     if bayes:
         arrs["ode_eps"] = ode_eps.numpy()
@@ -317,7 +337,7 @@ def make_e2e_case(name, R, n_qs, B, S_, window, gamma, ode_params, enc_params, s
     dist = {k: normwise_rel(o32[k], o64[k]) for k in o64}
     meta = {"B": B, "window": window, "gamma": gamma, "n_qs": n_qs, "n_regions": R, "n_samples": S_, "bayes": bayes,
             "losses": losses, "loss_names": names, "loss_data": data, "ode_params": ode_params,
-            "enc_params": enc_params, "ref32_vs_ref64": dist,
+            "enc_params": enc_params, "ref32_vs_ref64": dist, "ref32b_vs_ref64": dist_b,
             "generator": "tests/golden/make_golden.py make_e2e_case (reference lib/VAE.py + lib/models.py, "
                          "oracle RK4 as torchdiffeq), fp32 and fp64 runs of the reference step"}
     arrs["meta_json"] = np.array(json.dumps(meta))

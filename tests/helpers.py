@@ -75,14 +75,17 @@ class EvalMaskRecorder:
     time (a forward pre-hook): ``masks`` (E, N, R, 3) bool on the host after ``close``."""
 
     def __init__(self, mod):
-        self._m = []
+        self._m, self._g = [], []
         self._h = mod.register_forward_pre_hook(self._hook)
 
     def _hook(self, mod, args):
         x = args[1].detach()[..., :3]
         self._m.append(((x > 2) | (x < -1)).cpu())
+        self._g.append(torch.minimum((x - 2).abs(), (x + 1).abs()).reshape(x.shape[0], -1).amin(1).cpu())
 
     def close(self):
+        """(masks (E, N, R, 3), margin (N,): each trajectory's closest approach to the boundary)"""
         self._h.remove()
         self.masks = torch.stack(self._m)
+        self.margin = torch.stack(self._g).amin(0)
         return self.masks

@@ -88,7 +88,7 @@ def _bayes_pair(pkg, mod, y0, t, h, eps, dl):
     errs = {k: normwise_rel(fused[k], per[k]) for k in ("latent", "mean", "std", "fa_norm", "y0")}
     errs["d_mean"] = max(normwise_rel(a, b) for a, b in zip(fused["mu"], per["mu"]))
     errs["d_std"] = max(normwise_rel(a, b) for a, b in zip(fused["sd"], per["sd"]))
-    return fused, per, errs, agreeing_trajectories(mf, mp)
+    return fused, per, errs, agreeing_trajectories(mf, mp), rec.margin
 
 
 @pytest.mark.timeout(900)
@@ -106,13 +106,16 @@ def test_bayes_state49_full_batch(pkg):
     eps = torch.randn(4 * (n_t - 1), n_par, generator=gen)
     dl = torch.randn((n_t, N, 49, 8), generator=gen).to(DEV)
     assert pkg.fusable(mod, y0.to(DEV))
-    fused, per, errs, agree = _bayes_pair(pkg, mod, y0, t, h, eps, dl)
+    fused, per, errs, agree, margin = _bayes_pair(pkg, mod, y0, t, h, eps, dl)
     K = int(agree.sum())
+    far = agree & (margin > 1e-3)
     rows = {"latent": normwise_rel(fused["latent"][:, agree], per["latent"][:, agree]),
-            "y0": normwise_rel(fused["y0"][agree], per["y0"][agree])}
+            "y0": normwise_rel(fused["y0"][agree], per["y0"][agree]),
+            "y0_far": normwise_rel(fused["y0"][far], per["y0"][far])}
     print(f"bayes_state49 full batch, whole-solve vs per-evaluation kernels: "
           + ", ".join(f"{k} {v:.2e}" for k, v in errs.items())
-          + f"; {K}/{N} trajectories decide alike: latent {rows['latent']:.2e}, y0 {rows['y0']:.2e}")
+          + f"; {K}/{N} trajectories decide alike: latent {rows['latent']:.2e}, y0 {rows['y0']:.2e}; "
+          f"{int(far.sum())} of them stay 1e-3 away from the boundary: y0 {rows['y0_far']:.2e}")
     # a 256-row slice from the middle of the batch against the fp64 oracle (same eps rows)
     sl = torch.arange(N // 2 - 128, N // 2 + 128)
     mod.cpu()
@@ -121,13 +124,15 @@ def test_bayes_state49_full_batch(pkg):
     e_slice = normwise_rel(fused["latent"][:, sl], ref["latent"])
     print(f"  256-row slice latent vs fp64 {e_slice:.2e}")
     assert e_slice <= 1e-5
-    assert K >= N - 64, K
-    assert rows["latent"] <= 1e-6 and rows["y0"] <= 1e-5, rows
-    if K < N:
-        mod = mod.to(DEV)
-        fused, per, errs, agree2 = _bayes_pair(pkg, mod, y0[agree].contiguous(), t, h, eps, dl[:, agree].contiguous())
-        print("  agreeing trajectories as one batch: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
-        assert bool(agree2.all())
+    assert K >= N - 64 and int(far.sum()) >= 1000, (K, int(far.sum()))
+    # rows: the latent of every agreeing trajectory; dy0 of those that keep 1e-3 away from the mask
+    # boundary (next to it fp32 rounding alone moves the gradient, test_north_star)
+    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 1e-5, rows
+    # the batch sums (posterior, |Fa|, every d mean / d std) over the trajectories that keep away from it
+    mod = mod.to(DEV)
+    fused, per, errs, agree2, _ = _bayes_pair(pkg, mod, y0[far].contiguous(), t, h, eps, dl[:, far].contiguous())
+    print(f"  the {int(far.sum())} as one batch: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert bool(agree2.all())
     for k in ("latent", "mean", "std", "fa_norm"):
         assert errs[k] <= 1e-6, (k, errs[k])
     assert errs["y0"] <= 1e-5 and errs["d_mean"] <= 5e-5 and errs["d_std"] <= 5e-5, errs
@@ -225,18 +230,21 @@ def test_adjoint_state49_full_batch(pkg):
         return [yg.grad.clone()] + [p.grad.clone() for p in params]
 
     adj = lambda yg: odeint_adjoint(mod, yg, t)
+    rk4 = lambda h: (lambda yg: pkg.odeint(mod, yg, t, method="rk4", options=dict(step_size=h)))
     a1 = run(adj)
     info = dict(mod.last_adjoint_info)
     a2 = run(adj)
-    fine = run(lambda yg: pkg.odeint(mod, yg, t, method="rk4", options=dict(step_size=1.0 / 32)))
+    fine, finer = run(rk4(1.0 / 32)), run(rk4(1.0 / 64))
     assert info["fused"], info
     assert all(torch.equal(x, y) for x, y in zip(a1, a2))
     errs = [normwise_rel(x, y) for x, y in zip(a1, fine)]
+    # the fine-step reference's own discretisation error: the rate net's output is |q| (lib/models.py:134),
+    # not differentiable where q crosses 0, which drops BPTT through RK4 to first order in h for the
+    # rate-net weights (measured in fp64 on the host: h = 1/32 vs 1/64 differ by 2.6e-4 there, 3e-8 for
+    # the A-net and dy0)
+    disc = [normwise_rel(x, y) for x, y in zip(fine, finer)]
     names = ["y0"] + [f"{n}.{w}" for n, lin in enumerate(mod.ude_linears()) for w in ("weight", "bias")]
-    print(f"adjoint full batch ({info}): vs fine-step RK4 backprop " +
-          ", ".join(f"{n} {e:.1e}" for n, e in zip(names, errs)))
-    # dy0: per-trajectory adjoint states; the parameter adjoint a_theta is one fp32 vector integrated over
-    # every accepted step of the backward solve (sums over 20,480 trajectories per evaluation, with
-    # cancellation), the fp32 accumulation bound of which is ~steps x 6e-8
-    assert errs[0] <= 1e-5, errs[0]
-    assert max(errs[1:]) <= 1e-3, errs
+    print(f"adjoint full batch ({info}): vs fine-step RK4 backprop (h=1/32 vs 1/64 in brackets) " +
+          ", ".join(f"{n} {e:.1e} [{d:.1e}]" for n, e, d in zip(names, errs, disc)))
+    for n, e, d in zip(names, errs, disc):
+        assert e <= max(1e-5, 3.0 * d), (n, e, d)

@@ -131,7 +131,7 @@ def test_materialized_lists_bayes(pkg, R):
     out = []
     for m, dev, mat in ((mod, "cuda", True), (mod_c, "cpu", False), (mod, "cuda", False)):
         m.set_eps_stream(eps.to(dev))
-        out.append(_solve(pkg, m, y0.to(dev).requires_grad_(True), t, mat))
+        out.append(_solve(pkg, m, y0.detach().to(dev).requires_grad_(True), t, mat))
     (p_f, tr_f, post_f, nrm_f, g_f), (p_e, tr_e, post_e, nrm_e, g_e), (_, _, _, _, g_s) = out
     assert len(p_f) == len(p_e) == 4 * (len(t) - 1) == len(tr_f) == len(tr_e)
     for a, b in zip(p_f + tr_f, p_e + tr_e):

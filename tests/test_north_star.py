@@ -90,11 +90,14 @@ def _scale_outputs(mod, sp, sa):
                 getattr(mod, name)[-1].bias.mul_(s)
 
 
-def _oracle(mod, y0, t, dl, dtype, stats=True, masks=True, chunk=512):
+def _oracle(mod, y0, t, dl, dtype, stats=True, masks=True, chunk=512, k_order="torch"):
     """The chunked oracle (oracle/ude_oracle.py solve_and_grad_chunked) in ``dtype`` on spawned
-    CPU workers: latent, posterior / |Fa|, every gradient, every evaluation's mask decisions."""
+    CPU workers: latent, posterior / |Fa|, every gradient, every evaluation's mask decisions.
+    k_order="rev4": the same arithmetic with every Linear's products summed in another order."""
     dm, ds, dn = (DM.to(dtype), DS.to(dtype), DN) if stats else (None, None, None)
-    return solve_and_grad_chunked(OracleRHS.from_module(mod, dtype), y0.to(dtype), t, t[1] - t[0],
+    rhs = OracleRHS.from_module(mod, dtype)
+    rhs.k_order = k_order
+    return solve_and_grad_chunked(rhs, y0.to(dtype), t, t[1] - t[0],
                                   None if dl is None else dl.to(dtype), dm, ds, dn, chunk=chunk,
                                   workers=WORKERS, masks=masks)
 
@@ -118,6 +121,9 @@ def _fmt(d):
 
 
 STAT_KEYS = ("latent", "mean", "std", "fa_norm")
+# closest approach of a trajectory's stage inputs to the mask boundary below which its gradient is
+# treated as ill-conditioned (fp32 rounding alone moves it by more than the 2e-5 bar there)
+MARGIN = 1e-3
 
 
 def _assert_bars(errs, label, mod, y0, t, dl, names):
@@ -162,10 +168,7 @@ def _full_batch(pkg, mod, y0, t, dl, label, fp32_whole=False):
     if fp32_whole:
         r32 = _oracle(mod, y0, t, dl, torch.float32)
         o32 = _res_dict(r32, names)
-        # the same fp32 arithmetic with other GEMM blockings (chunks of 128 trajectories instead of
-        # 512): how far apart two fp32 roundings of the reference's own computation land
-        r32.alt = _res_dict(_oracle(mod, y0, t, dl, torch.float32, masks=False, chunk=128), names)
-        lines.append("  whole batch, fp32 oracle (128-trajectory chunks) vs fp64: " + _fmt(_errs(r32.alt, ref)))
+
         agree32 = agreeing_trajectories(r32.masks, r64.masks)
         k32 = int(agree32.sum())
         lines.append(f"  fp32 oracle: {k32}/{N} trajectories agree with fp64; the kernel and the fp32 "
@@ -202,6 +205,22 @@ def _full_batch(pkg, mod, y0, t, dl, label, fp32_whole=False):
         if int(far.sum()):
             lines.append(f"  agreeing with margin > {thr:g}: {int(far.sum())} trajectories, dy0 "
                          f"{normwise_rel(got['y0'][far], r64.grads['y0'][far]):.2e}")
+    split["near"] = agree & ~(r64.margin > MARGIN)
+    split["far"] = agree & (r64.margin > MARGIN)
+    if fp32_whole and int(split["near"].sum()):
+        # the agreeing trajectories that come within MARGIN of the mask boundary: the same fp32
+        # arithmetic with another summation order (k_order rev4) samples how far fp32 rounding moves
+        # their (ill-conditioned) gradients
+        nb = split["near"]
+        # (their own batch, the latent term of the loss only: fp32 orders against fp64 of the same loss)
+        yn, dn = y0[nb].contiguous(), dl[:, nb].contiguous()
+        alt = _oracle(mod, yn, t, dn, torch.float32, stats=False, masks=False, k_order="rev4")
+        alt64 = _oracle(mod, yn, t, dn, torch.float64, stats=False, masks=False)
+        r32.near_alt = normwise_rel(alt.grads["y0"], alt64.grads["y0"])
+        lines.append(f"  the {int(nb.sum())} agreeing trajectories within {MARGIN:g} of the boundary: dy0 kernel "
+                     f"{normwise_rel(got['y0'][nb], r64.grads['y0'][nb]):.2e}, fp32 oracle "
+                     f"{normwise_rel(r32.grads['y0'][nb], r64.grads['y0'][nb]):.2e}, fp32 oracle in another "
+                     f"summation order {r32.near_alt:.2e}")
     print("\n".join(lines))
     return got, ref, r32, agree, names, whole, split
 
@@ -254,10 +273,16 @@ def test_north_star_m1_full_size(pkg, kind, net, aug, sa):
         assert whole["latent"] <= bar, f"whole-batch latent {whole['latent']:.3e} > 2 x the fp32 oracle's {bar / 2:.3e}"
     assert int(agree.sum()) >= 16, "too few agreeing trajectories for the gradient check"
     assert split["latent"] <= 1e-5, split
-    # dy0 of the agreeing trajectories: <= max(2e-5, 2 x the farther of the two fp32 oracle runs)
-    bar = max(2e-5, 2.0 * max(normwise_rel(r32.grads["y0"][agree], ref["y0"][agree]),
-                              normwise_rel(r32.alt["y0"][agree], ref["y0"][agree])))
-    assert split["y0"] <= bar, (split, bar)
+    # dy0: the agreeing trajectories that keep their distance from the boundary <= 2e-5; those that come
+    # within MARGIN of it <= max(2e-5, 2 x the farther of two fp32 roundings of the reference arithmetic)
+    far = split["far"]
+    e_far = normwise_rel(got["y0"][far], ref["y0"][far])
+    assert int(far.sum()) >= 16 and e_far <= 2e-5, (int(far.sum()), e_far)
+    nb = split["near"]
+    if int(nb.sum()):
+        e_nb = normwise_rel(got["y0"][nb], ref["y0"][nb])
+        bar = max(2e-5, 2.0 * max(normwise_rel(r32.grads["y0"][nb], ref["y0"][nb]), r32.near_alt))
+        assert e_nb <= bar, (e_nb, bar)
     _agreeing_batch(pkg, mod, y0, t, dl, agree, names, label)
 
 

@@ -705,20 +705,27 @@ __global__ __launch_bounds__(256) void ude_nll_bwd_kernel(const float* __restric
   const int gid = blockIdx.x * 256 + threadIdx.x;
   if (gid >= T * B * R) return;
   const int r = gid % R, tb = gid / R, b = tb % B, t = tb / B;
-  const float mu = musd[(size_t)gid * 2], sd = musd[(size_t)gid * 2 + 1];
+  const float sd = musd[(size_t)gid * 2 + 1];
   const float yv = y[((size_t)b * T + t) * R + r];
+  const size_t stride = (size_t)B * R;
+  const size_t base = (size_t)t * S * stride + (size_t)b * R + r;
+  // the group mean again in fp64: the std term's cotangent cs * (yhat_s - mean) is large (cs ~ dy^2 /
+  // sd^4 when the prediction misses by many sd) and its sum over the samples cancels to ~0, so a mean
+  // rounded to fp32 (|mean| >> sd) leaves a residual S * ulp(mean) * cs in every reduction of d yhat
+  // (the decoder's bias / weight gradients)
+  double m64 = 0.0;
+  for (int s = 0; s < S; ++s) m64 += (double)yhat[base + s * stride];
+  m64 /= (double)S;
   float cm = 0.f, cs = 0.f;
   if (yv != -1.f) {
-    const float iv = 1.f / sd, dy = yv - mu;
+    const float iv = 1.f / sd, dy = (float)((double)yv - m64);
     const float dmu = -dy * iv * iv;
     const float dsd = iv - dy * dy * iv * iv * iv;
     const float sc = (float)((double)grad[0] / ((double)B * T * R));
     cm = sc * dmu / (float)S;
     cs = sc * dsd * iv / (float)(S - 1);
   }
-  const size_t stride = (size_t)B * R;
-  const size_t base = (size_t)t * S * stride + (size_t)b * R + r;
-  for (int s = 0; s < S; ++s) dyhat[base + s * stride] = cm + cs * (yhat[base + s * stride] - mu);
+  for (int s = 0; s < S; ++s) dyhat[base + s * stride] = cm + cs * (float)((double)yhat[base + s * stride] - m64);
 }
 
 }  // namespace ude

@@ -164,7 +164,7 @@ class FusedRK4(torch.autograd.Function):
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
-        sums = stats_slab[:5].clone()
+        sums = stats_slab[:5]
         ctx.mark_non_differentiable(out_ck, sums)
         return latent, stats, out_ck, sir_token_like(latent), sums
 
@@ -298,7 +298,7 @@ def _dec_forward(plan: Plan, y0: torch.Tensor, pack: torch.Tensor, Wd: torch.Ten
                          reg_slab.data_ptr(), stats.data_ptr(), reg.data_ptr(), stream)
     if EVENTS is not None:
         e1 = _ev(dev); e1.record(); EVENTS.append(("fwd_dec", e0, e1))
-    return yhat, reg, stats, ckpt, stats_slab[:5].clone()
+    return yhat, reg, stats, ckpt, stats_slab[:5]
 
 
 def _dec_backward(plan: Plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent):
@@ -453,7 +453,7 @@ class FusedBayesRK4(torch.autograd.Function):
         ctx.plan = plan
         if need_grad:
             ctx.save_for_backward(y0, pack, ckpt, stats, *sds)
-        sums = stats_slab[:5].clone()
+        sums = stats_slab[:5]
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(out_ck, sums)
         return latent, stats, out_ck, sums

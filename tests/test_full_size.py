@@ -125,9 +125,10 @@ def test_bayes_state49_full_batch(pkg):
     print(f"  256-row slice latent vs fp64 {e_slice:.2e}")
     assert e_slice <= 1e-5
     assert K >= N - 64 and int(far.sum()) >= 1000, (K, int(far.sum()))
-    # rows: the latent of every agreeing trajectory; dy0 of those that keep 1e-3 away from the mask
-    # boundary (next to it fp32 rounding alone moves the gradient, test_north_star)
-    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 1e-5, rows
+    # rows: the latent of every agreeing trajectory (1e-6); dy0 of those that keep 1e-3 away from the mask
+    # boundary (next to it fp32 rounding alone moves the gradient, test_north_star), 2e-5 as the
+    # fp32-vs-fp64 bar (two fp32 implementations)
+    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 2e-5, rows
     # the batch sums (posterior, |Fa|, every d mean / d std) over the trajectories that keep away from it
     mod = mod.to(DEV)
     fused, per, errs, agree2, _ = _bayes_pair(pkg, mod, y0[far].contiguous(), t, h, eps, dl[:, far].contiguous())

@@ -1,0 +1,14 @@
+# Round-4: re-run the fixed full-size / e2e tests, then a per-kernel trace of the default bench step.
+set -o pipefail
+export TMPDIR=/tmp
+R=$(pwd)
+mkdir -p gpurun_out/r04
+O=$R/gpurun_out/r04
+timeout -k 10 900 python -u -m pytest tests/test_north_star.py tests/test_full_size.py tests/test_e2e_vae.py -v -s -m gpu --timeout 800 --timeout-method thread -k "m1_full_size or bayes_state49 or us_bayes or test_vae_step_fused" > $O/pytest_full4.log 2>&1
+rc=$?
+grep -E "passed|failed" $O/pytest_full4.log | tail -3
+cd /tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks1 -o ks -- python3 $R/bench.py --no-extra --no-cpu-baseline --steps 5 --warmup 2 > $O/ks_state49.log 2>&1 || exit 11
+find /tmp/ks1 -name "*kernel_stats.csv" -exec cp {} $O/state49_kernel_stats.csv \;
+find /tmp/ks1 -name "*kernel_trace.csv" -exec cp {} $O/state49_kernel_trace.csv \;
+exit $rc

@@ -353,9 +353,13 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     hook(dd);
     __builtin_amdgcn_sched_barrier(0);
     f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
+    // one output tile in this phase: its K chain as two interleaved accumulators (see mlp_backward)
+    constexpr bool DUALF = M::own_phase(W, d) == 1 && M::kin(M::fnet(d, M::first_owned(W, d)), d) >= 32;
+    f4 acc2[DUALF ? M::FT(d) : 1];
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
+        if constexpr (DUALF) acc2[k] = f4zero();
         if constexpr (d == 0 && M::HOIST) acc[k] = c1[M::nz_before(W, k)];
         else if constexpr (RW) acc[k] = wr.wb[M::nb_base(W, d) + M::nb_before(W, d, k)];
         else acc[k] = bias[k];
@@ -406,8 +410,9 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
                   f4 wq;
                   if constexpr (CHUNK_A) wq = fa[cb][CHUNK_A ? k : 0][CHUNK_A ? q - q0 : 0];
                   else wq = FR(M::fq_before(W, d, k) + q);
-                  if constexpr (UDE_ABL != 13) acc[k] = mfma4(wq[e], x[e], acc[k]);
-                  else acc[k][e] += x[e];
+                  if constexpr (UDE_ABL == 13) acc[k][e] += x[e];
+                  else if (DUALF && (e & 1)) acc2[DUALF ? k : 0] = mfma4(wq[e], x[e], acc2[DUALF ? k : 0]);
+                  else acc[k] = mfma4(wq[e], x[e], acc[k]);
                 }
               });
           }
@@ -419,6 +424,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
       if constexpr (M::fowner(d, k) == W) {
         constexpr int net = M::fnet(d, k), rt = M::frt(d, k);
         f4 a = acc[k];
+        if constexpr (DUALF) a = a + acc2[k];
         if constexpr (M::act(net, d)) {
           a[0] = elu1(a[0]); a[1] = elu1(a[1]);
           a[2] = elu1(a[2]); a[3] = elu1(a[3]);
@@ -1120,10 +1126,16 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       return;
     }
     f4 avv[M::XT(d) > 0 ? M::XT(d) : 1];
+    // a wave with a single input-gradient tile in this phase runs its K chain as two interleaved
+    // accumulation chains (even / odd k quads): the chain is latency-bound there (40 cycles per
+    // dependent v_mfma_f32_16x16x4_f32 against a 32-cycle issue), with two it is issue-bound
+    constexpr bool DUALX = M::own_x(W, d) == 1;
+    f4 xo[DUALX ? M::XT(d) : 1];
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
         xa[m] = f4zero();
+        if constexpr (DUALX) xo[m] = f4zero();
         if constexpr (d > 0) {
           // the ELU-derivative operand of the epilogue, read ahead of the MFMAs
           constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
@@ -1150,9 +1162,11 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
           for (int e = 0; e < 4; ++e)
             sfor<M::XT(d)>([&](auto mm) {
               constexpr int m = decltype(mm)::value;
-              if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net))
-                if constexpr (UDE_ABL != 3) xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
-                else xa[m][e] += x[e];
+              if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net)) {
+                if constexpr (UDE_ABL == 3) xa[m][e] += x[e];
+                else if (DUALX && (e & 1)) xo[DUALX ? m : 0] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xo[DUALX ? m : 0]);
+                else xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
+              }
             });
         }
       }
@@ -1162,6 +1176,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
         f4 acc = xa[m];
+        if constexpr (DUALX) acc = acc + xo[m];
         if constexpr (d == 0) {
           ep0(m * 16 + g * 4, acc);
         } else {

@@ -109,7 +109,10 @@ struct Model {
   // (R = 1 at the reference's sizes).  Larger Bayesian models (GST) store each evaluation's
   // layer-output gradient rows instead and a separate kernel (ude_gst_dw_kernel) forms every
   // evaluation's weight gradient as one GEMM over the whole batch, eps-weighting it there.
-  static constexpr bool GST = BAYES && max_ndw() > 20;
+#ifndef UDE_GST_MIN_NDW
+#define UDE_GST_MIN_NDW 20
+#endif
+  static constexpr bool GST = BAYES && max_ndw() > UDE_GST_MIN_NDW;
   static constexpr bool FITS = true;
   // ---- LDS record: one row of SR floats per trajectory ([t][feature]) ---------
   static constexpr int Y_OFF = 0;
@@ -303,6 +306,16 @@ struct Model {
     int s = 0;
     for (int k = 0; k < FT(d); ++k) if (fowner(d, k) == w) s += 1;
     return s;
+  }
+  // input-gradient tiles wave w owns in phase d; its first owned forward tile of phase d (0 if none)
+  static constexpr int own_x(int w, int d) {
+    int s = 0;
+    for (int m = 0; m < XT(d); ++m) if (xowner(d, m) == w) s += 1;
+    return s;
+  }
+  static constexpr int first_owned(int w, int d) {
+    for (int k = 0; k < FT(d); ++k) if (fowner(d, k) == w) return k;
+    return 0;
   }
   static constexpr int nz_before(int w, int k) {
     int s = 0;

@@ -11,4 +11,7 @@ cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks1 -o ks -- python3 $R/bench.py --no-extra --no-cpu-baseline --steps 5 --warmup 2 > $O/ks_state49.log 2>&1 || exit 11
 find /tmp/ks1 -name "*kernel_stats.csv" -exec cp {} $O/state49_kernel_stats.csv \;
 find /tmp/ks1 -name "*kernel_trace.csv" -exec cp {} $O/state49_kernel_trace.csv \;
+cd $R
+timeout -k 10 300 python -u tools/ab_gst_r1.py > $O/ab_gst_r1.log 2>&1 || exit 12
+cat $O/ab_gst_r1.log
 exit $rc

@@ -106,11 +106,15 @@ struct Model {
   }
   static constexpr int max_ndw() { return cmax(cmax(NDW(0), NDW(1)), cmax(NDW(2), NDW(3))); }
   // BAYES keeps a second (eps-weighted) accumulator per dW tile in registers when both sets fit
-  // (R = 1 at the reference's sizes).  Larger Bayesian models (GST) store each evaluation's
-  // layer-output gradient rows instead and a separate kernel (ude_gst_dw_kernel) forms every
-  // evaluation's weight gradient as one GEMM over the whole batch, eps-weighting it there.
+  // and are small (the models_bayes.py class defaults, the R = 1 Fp / Fa nets).  Larger Bayesian
+  // models (GST) store each evaluation's layer-output gradient rows instead and a separate kernel
+  // (ude_gst_dw_kernel) forms every evaluation's weight gradient as one GEMM over the whole batch,
+  // eps-weighting it there.  Above 12 dW tiles per wave GST wins even at R = 1: the US FaFp
+  // [64,64,32]/[64,64] model (16) measured bwd 12.48 -> 10.33 ms, step 18.84 -> 17.16 ms on the
+  // 4,096 x 365-step bayes_us workload (fwd 5.78 -> 6.13: it stores the stage inputs too;
+  // tools/ab_gst_r1.py, profiles/r04/ab_gst_r1.log).
 #ifndef UDE_GST_MIN_NDW
-#define UDE_GST_MIN_NDW 20
+#define UDE_GST_MIN_NDW 12
 #endif
   static constexpr bool GST = BAYES && max_ndw() > UDE_GST_MIN_NDW;
   static constexpr bool FITS = true;

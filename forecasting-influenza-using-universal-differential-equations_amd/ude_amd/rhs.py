@@ -132,8 +132,11 @@ class _UDEModule(nn.Module):
         statistics exchange (distributed.sync_side_stats)."""
         if sums is not None and evals is None:
             self._fused_sums.append((float(n_eval), stats, sums))
+        # one split node: its backward concatenates the three cotangents into d stats (three slice
+        # nodes each zero-filled, copied and accumulated a 5-vector: eight small kernels per step)
+        s_mean, s_std, s_fa = stats.split([2, 2, 1])
         if self.ode_type in ("Fp", "FaFp"):
-            self._fused_rates.append((float(n_eval), stats[0:2], stats[2:4]))
+            self._fused_rates.append((float(n_eval), s_mean, s_std))
             if evals is not None:
                 if not isinstance(self.params, _FusedList):
                     self.params = _FusedList(self.params)
@@ -146,7 +149,7 @@ class _UDEModule(nn.Module):
             else:
                 # torch.norm(torch.stack(tracker)) over this entry == |Fa| of the solve,
                 # and over several entries == the norm of all of them together.
-                self.tracker.append(stats[4:5])
+                self.tracker.append(s_fa)
 
     @torch.no_grad()
     def _evals_from_checkpoint(self, ckpt: torch.Tensor, y0: torch.Tensor, n_steps: int, chunk: int = 64):

@@ -124,19 +124,32 @@ def test_bayes_state49_full_batch(pkg):
     e_slice = normwise_rel(fused["latent"][:, sl], ref["latent"])
     print(f"  256-row slice latent vs fp64 {e_slice:.2e}")
     assert e_slice <= 1e-5
+    # dy0 of 256 well-conditioned trajectories (agreeing, 1e-3 from the boundary) solved as a batch of
+    # their own on the whole-solve kernels against the fp64 Bayes oracle (latent cotangent only)
+    fs = torch.nonzero(far).flatten()[:256]
+    yk, dk = y0[fs].contiguous(), dl[:, fs].double().cpu().contiguous()
+    refk = solve_and_grad_bayes(OracleBayesRHS.from_module(mod, torch.float64), eps.double(), yk.double(), t, h, dk)
+    mod = mod.to(DEV)
+    yg = yk.to(DEV).requires_grad_(True)
+    mod.clear_tracking()
+    mod.set_eps_stream(eps.to(DEV))
+    (pkg.odeint(mod, yg, t, method="rk4", options=dict(step_size=h)).double() * dk.to(DEV)).sum().backward()
+    e_dy0 = normwise_rel(yg.grad, refk["grads"]["y0"])
+    print(f"  {len(fs)} well-conditioned trajectories, whole-solve kernels vs fp64: dy0 {e_dy0:.2e}")
+    assert e_dy0 <= 2e-5
+    mod.zero_grad(set_to_none=True)
     assert K >= N - 64 and int(far.sum()) >= 1000, (K, int(far.sum()))
     # rows: the latent of every agreeing trajectory (1e-6); dy0 of those that keep 1e-3 away from the mask
-    # boundary (next to it fp32 rounding alone moves the gradient, test_north_star), 2e-5 as the
-    # fp32-vs-fp64 bar (two fp32 implementations)
-    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 2e-5, rows
+    # boundary (next to it fp32 rounding alone moves the gradient, test_north_star): 4e-5 between the two
+    # fp32 paths, each held to 2e-5 of fp64 (the whole-solve one on the slice above)
+    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 4e-5, rows
     # the batch sums (posterior, |Fa|, every d mean / d std) over the trajectories that keep away from it
-    mod = mod.to(DEV)
     fused, per, errs, agree2, _ = _bayes_pair(pkg, mod, y0[far].contiguous(), t, h, eps, dl[:, far].contiguous())
     print(f"  the {int(far.sum())} as one batch: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     assert bool(agree2.all())
     for k in ("latent", "mean", "std", "fa_norm"):
         assert errs[k] <= 1e-6, (k, errs[k])
-    assert errs["y0"] <= 1e-5 and errs["d_mean"] <= 5e-5 and errs["d_std"] <= 5e-5, errs
+    assert errs["y0"] <= 4e-5 and errs["d_mean"] <= 5e-5 and errs["d_std"] <= 5e-5, errs
 
 
 @pytest.mark.timeout(1200)

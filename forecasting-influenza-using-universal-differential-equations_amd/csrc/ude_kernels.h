@@ -96,6 +96,19 @@ __device__ __forceinline__ float reg_term(float v) {
 #ifndef UDE_ABL
 #define UDE_ABL 0
 #endif
+// Two interleaved accumulation chains for a wave's single-tile forward / input-gradient phases
+// (-DUDE_DUAL=1).  Off: measured no gain (tools/ab_flags.py, profiles/r04/ab_dual_*.log: M1 Fp [32,32]
+// 3.203 vs 3.196 ms/step, M1 FaFp 7.642 vs 7.623, state49 2.897 vs 2.884 with / without), and it
+// changes the fp32 summation order of those phases
+#ifndef UDE_DUAL
+#define UDE_DUAL 0
+#endif
+// Training forward (large records, 4 waves): each layer's activation rows go to HBM during the next
+// layer's phase, issued behind that phase's weight loads (-DUDE_FWD_EARLY_ST=0: all rows after the
+// stage's last phase, the A/B baseline)
+#ifndef UDE_FWD_EARLY_ST
+#define UDE_FWD_EARLY_ST 1
+#endif
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
@@ -354,7 +367,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     __builtin_amdgcn_sched_barrier(0);
     f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
     // one output tile in this phase: its K chain as two interleaved accumulators (see mlp_backward)
-    constexpr bool DUALF = M::own_phase(W, d) == 1 && M::kin(M::fnet(d, M::first_owned(W, d)), d) >= 32;
+    constexpr bool DUALF = UDE_DUAL && M::own_phase(W, d) == 1 && M::kin(M::fnet(d, M::first_owned(W, d)), d) >= 32;
     f4 acc2[DUALF ? M::FT(d) : 1];
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
@@ -510,6 +523,34 @@ __host__ __device__ __forceinline__ int act_src_q(int i) {
   else return (i / QR) * (M::XST_W / 4) + M::ACT_IN / 4 + (i - (i / QR) * QR);
 }
 
+// Record columns [ACT0 + 4 LQ, ACT0 + 4 (LQ + NQL)) of the tile's 16 trajectories -> their stored
+// activation rows (one layer's outputs; 16-B LDS reads, 16-B global stores).
+template <class M, int SR, int LQ, int NQL>
+__device__ __forceinline__ void store_act_cols(float* blk, const float* lds, int tid) {
+  constexpr int PER = (TT * NQL + NTHREADS - 1) / NTHREADS;
+  f4* dst = reinterpret_cast<f4*>(blk);
+  // thread-derived addresses formed here, not hoisted out of the stage loop into registers the
+  // layer phases need (the forward is at the 256-VGPR limit)
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + u * NTHREADS;
+    if (i < TT * NQL) {
+      const int t = i / NQL, q = LQ + (i - t * NQL);
+      dst[t * (M::XST_W / 4) + M::ACT_IN / 4 + q] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
+    }
+  }
+}
+// layer j's rows of every net that has a layer j
+template <class M, int SR, int J>
+__device__ __forceinline__ void store_act_layer(float* blk, const float* lds, int tid) {
+  sfor<2>([&](auto nn) {
+    constexpr int net = decltype(nn)::value;
+    if constexpr (J < M::nl(net))
+      store_act_cols<M, SR, (M::act_off(net, J) - M::ACT0) / 4, M::kout(net, J) / 4>(blk, lds, tid);
+  });
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -648,12 +689,24 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         if constexpr (PFB) {
           if (step == 0 && j == 0) wr.load(rse, lane, false);        // the tile's first evaluation
         }
-        mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
+        constexpr bool EARLY_ST = TRAIN && M::ACT_STORED && !SPLIT && !M::STORE_ACT && UDE_FWD_EARLY_ST && UDE_ABL != 11;
+        if constexpr (EARLY_ST) {
+          // layer d - 1's rows during phase d, behind its weight loads: a later wait on those loads
+          // (in-order vmcnt) then does not also wait for these stores to complete
+          float* blk = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j);
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, nullptr, [&](auto dd) {
+            constexpr int d = decltype(dd)::value;
+            if constexpr (d >= 1) store_act_layer<M, SR, d - 1>(blk, lds, tid);
+          });
+          store_act_layer<M, SR, M::D - 1>(blk, lds, tid);
+        } else {
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
+        }
         if constexpr (PFB) {
           const int en = 4 * step + j + 1;
           if (en < 4 * A.n_steps) wr.load(make_rsrc(A.pack + (size_t)en * M::PACK_TOTAL, M::PACK_TOTAL * 4), lane, false);
         }
-        if constexpr (TRAIN && M::ACT_STORED && !SPLIT && UDE_ABL != 11) {
+        if constexpr (TRAIN && M::ACT_STORED && !SPLIT && !EARLY_ST && UDE_ABL != 11) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
@@ -1129,7 +1182,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
     // a wave with a single input-gradient tile in this phase runs its K chain as two interleaved
     // accumulation chains (even / odd k quads): the chain is latency-bound there (40 cycles per
     // dependent v_mfma_f32_16x16x4_f32 against a 32-cycle issue), with two it is issue-bound
-    constexpr bool DUALX = M::own_x(W, d) == 1;
+    constexpr bool DUALX = UDE_DUAL && M::own_x(W, d) == 1;
     f4 xo[DUALX ? M::XT(d) : 1];
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;

@@ -90,3 +90,41 @@ def test_two_rank_dp_matches_single_process(pkg, materialize):
         assert torch.allclose(rn, nrm.cpu().reshape(1), rtol=1e-5)
         for a, b in zip(grads, ref):
             assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max())), float((a - b).abs().max())
+
+
+def _rccl_worker(port, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        dev = torch.device("cuda", 0)
+        # the payloads of ude_amd.distributed: the fp64 statistics totals (combine_sums), one flat
+        # fp32 gradient bucket (all_reduce_grads), parameter / RNG-state broadcasts
+        sums = torch.tensor([96.0, 1.5, -2.25, 3.0, 4.5, 0.75], dtype=torch.float64, device=dev)
+        flat = torch.randn(300_001, device=dev)
+        ref_s, ref_f = sums.clone(), flat.clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        dist.broadcast(flat, src=0)
+        torch.cuda.synchronize()
+        q.put((dist.get_backend(), torch.equal(sums, ref_s), torch.equal(flat, ref_f)))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", traceback.format_exc()))
+
+
+def test_rccl_single_rank_collectives():
+    """The RCCL backend ("nccl" on ROCm) on this box: a one-rank process group runs the collectives the
+    data-parallel path issues (fp64 statistics totals, the fp32 gradient bucket, a broadcast) through
+    RCCL.  The 1-GPU box cannot host a multi-rank RCCL group (one rank per GPU); the multi-rank
+    arithmetic is covered by the gloo tests above and the driver's multi-GPU bench."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(29800 + os.getpid() % 1000, q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] != "err", res[1]
+    assert res == ("nccl", True, True)

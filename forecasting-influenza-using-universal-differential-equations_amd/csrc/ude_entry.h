@@ -382,6 +382,9 @@ struct Ops {
     a.latent = latent; a.ckpt = ckpt; a.stats_slab = stats_slab;
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
+#ifdef UDE_PROFILE
+    a.prof = g_prof_buffer ? g_prof_buffer + (size_t)PROF_FWD_SLOT * NPROF : nullptr;   // behind the backward's
+#endif
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const bool res = !(ckpt && M::SPLIT_FWD && n_tiles <= cus) && fwd_res(n_tiles, cus);

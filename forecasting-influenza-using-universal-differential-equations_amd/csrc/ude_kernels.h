@@ -113,6 +113,7 @@ __device__ __forceinline__ float reg_term(float v) {
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
 constexpr int NPROF = 20;
+constexpr int PROF_FWD_SLOT = 4096;          // the training forward's rows start at workgroup slot 4096
 struct Prof {
   unsigned long long acc[NPROF];
   unsigned long long last;
@@ -591,6 +592,14 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   constexpr bool PFB = M::FWD_PFB;
   WRegs<M, W, false, true, RES || PFB> wr;
   if constexpr (!PFB) wr.load(rs, lane);
+  Prof prof_, *pf = nullptr;
+#ifdef UDE_PROFILE
+  if (TRAIN && A.prof && tid == 0) {
+    pf = &prof_;
+    for (int i = 0; i < NPROF; ++i) prof_.acc[i] = 0;
+    prof_.last = __builtin_amdgcn_s_memtime();
+  }
+#endif
 
   #pragma unroll 1
   for (int i = tid; i < TT * SR; i += NTHREADS) lds[i] = 0.f;
@@ -675,6 +684,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
     lds_sync();
     if constexpr (DEC) dec_emit(0);               // output 0 = y0
+    UDE_STAMP(pf, 15);
 
     for (int step = 0; step < A.n_steps; ++step) {
       // DEC (R=49, at the 256-VGPR limit): the thread-derived 64-bit store addresses are recomputed
@@ -694,13 +704,13 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
           // layer d - 1's rows during phase d, behind its weight loads: a later wait on those loads
           // (in-order vmcnt) then does not also wait for these stores to complete
           float* blk = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j);
-          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, nullptr, [&](auto dd) {
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
             constexpr int d = decltype(dd)::value;
             if constexpr (d >= 1) store_act_layer<M, SR, d - 1>(blk, lds, tid);
           });
           store_act_layer<M, SR, M::D - 1>(blk, lds, tid);
         } else {
-          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr);
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf);
         }
         if constexpr (PFB) {
           const int en = 4 * step + j + 1;
@@ -725,6 +735,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             }
           }
         }
+        UDE_STAMP(pf, 0);
         if constexpr (UDE_ABL != 12) sfor<SL>([&](auto ss) {
           constexpr int sl = decltype(ss)::value;
           const int p = tid + sl * NTHREADS;
@@ -829,7 +840,9 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             }
           }
         });
+        UDE_STAMP(pf, 16);
         lds_sync();
+        UDE_STAMP(pf, 1);
       }
       if constexpr (DEC) {
         if (sc.out_start[step] < sc.out_start[step + 1]) dec_emit(sc.out_j[sc.out_start[step]]);
@@ -854,6 +867,9 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     if (tid < 5) A.stats_slab[(size_t)blockIdx.x * 5 + tid] = s;
     else A.reg_slab[blockIdx.x] = s;
   }
+#ifdef UDE_PROFILE
+  if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
+#endif
 }
 
 // Training forward of small records (Model::split_fwd): waves 4-7 store each stage's activation

@@ -4,6 +4,10 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r04
 O=gpurun_out/r04
+for wl in state49 us_northstar; do
+  timeout -k 10 150 python -u tools/stage_profile.py $wl > $O/stage_$wl.txt 2>&1 || { cat $O/stage_$wl.txt; exit 9; }
+  grep -v amdgpu.ids $O/stage_$wl.txt
+done
 for wl in state49 bayes_state49; do
   AB_WORKLOAD=$wl AB_VARIANTS="early1:;early0:-DUDE_FWD_EARLY_ST=0" timeout -k 10 300 python -u tools/ab_flags.py > $O/ab_early_$wl.log 2>&1 || { cat $O/ab_early_$wl.log; exit 11; }
   grep -v amdgpu.ids $O/ab_early_$wl.log

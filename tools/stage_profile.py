@@ -1,4 +1,4 @@
-"""Diagnostic: per-segment cycle breakdown of the backward kernel's stage loop.
+"""Diagnostic: per-segment cycle breakdown of the backward and training-forward kernels' stage loops.
 
 Builds a -DUDE_PROFILE copy of one configuration (s_memtime stamps at every
 barrier of the stage loop, thread 0 of each workgroup), runs the bench workload
@@ -24,6 +24,10 @@ SEG = {0: "stage input (ckpt)", 1: "barrier after ckpt", 2: "fwd d0", 3: "fwd d1
        12: "RK adjoint / split-x0 sum", 13: "step end (RK_A)", 14: "step start (cotangents)", 15: "tile start/end"}
 ORDER = [15, 14, 0, 1, 2, 3, 4, 5, 16, 17, 18, 6, 11, 10, 9, 8, 7, 12, 13]
 NPROF = 20
+FWD_SLOT = 4096                  # csrc PROF_FWD_SLOT: the training forward's rows
+FSEG = {15: "tile start/end", 2: "fwd d0 (+ barrier)", 3: "fwd d1 (+ barrier)", 4: "fwd d2 (+ barrier)",
+        5: "fwd d3 (+ barrier)", 0: "act rows (tail stores)", 16: "flux pass", 1: "barrier after flux"}
+FORDER = [15, 2, 3, 4, 5, 0, 16, 1]
 
 
 def main():
@@ -44,20 +48,24 @@ def main():
     mod, y0, t, dlat = bench.build(pkg, w, dev, seed=1)
     from ude_amd import distributed as udist
     bench.one_step(pkg, udist, mod, y0, t, dlat, 1)        # warm up (grid size known after)
-    buf = torch.zeros(4096 * NPROF, dtype=torch.int64, device=dev)
+    buf = torch.zeros(2 * FWD_SLOT * NPROF, dtype=torch.int64, device=dev)
     lib.lib.ude_debug_set_prof(buf.data_ptr())
     bench.one_step(pkg, udist, mod, y0, t, dlat, 1)
     torch.cuda.synchronize()
     lib.lib.ude_debug_set_prof(None)
-    v = buf.view(-1, NPROF).double()
-    used = v[v.sum(1) > 0]
     tiles = (w["n_traj"] + 15) // 16
-    stages = tiles * 4 * (len(t) - 1) / used.shape[0]
-    per = used.mean(0) / stages
-    tot = float(per.sum())
-    print(f"workgroups {used.shape[0]}, stages per WG {stages:.1f}, cycles per stage {tot:.0f}")
-    for k in ORDER:
-        print(f"  {SEG[k]:24s} {float(per[k]):9.0f}  {100 * float(per[k]) / tot:5.1f}%")
+    for name, rows, seg, order in (("backward", buf[:FWD_SLOT * NPROF], SEG, ORDER),
+                                   ("training forward", buf[FWD_SLOT * NPROF:], FSEG, FORDER)):
+        v = rows.view(-1, NPROF).double()
+        used = v[v.sum(1) > 0]
+        if used.shape[0] == 0:
+            continue
+        stages = tiles * 4 * (len(t) - 1) / used.shape[0]
+        per = used.mean(0) / stages
+        tot = float(per.sum())
+        print(f"{name}: workgroups {used.shape[0]}, stages per WG {stages:.1f}, cycles per stage {tot:.0f}")
+        for k in order:
+            print(f"  {seg[k]:24s} {float(per[k]):9.0f}  {100 * float(per[k]) / tot:5.1f}%")
 
 
 if __name__ == "__main__":

@@ -103,11 +103,16 @@ __device__ __forceinline__ float reg_term(float v) {
 #ifndef UDE_DUAL
 #define UDE_DUAL 0
 #endif
-// Training forward (large records, 4 waves): each layer's activation rows go to HBM during the next
-// layer's phase, issued behind that phase's weight loads (-DUDE_FWD_EARLY_ST=0: all rows after the
-// stage's last phase, the A/B baseline)
+// Training forward (large records, 4 waves), -DUDE_FWD_EARLY_ST=1: each layer's activation rows go to
+// HBM during the next layer's phase, issued behind that phase's weight loads.  Off: measured slower
+// (profiles/r04/ab_early_*.log: state49 fwd 1.075 vs 1.041 ms, Bayes state49 1.835 vs 1.742 ms) --
+// the stores then compete with the phases' weight and operand traffic instead of the flux pass
+// the forward's row-mapped tile start (fwd_tile_io); -DUDE_ROWS16=0: the per-pair copy loops (A/B)
+#ifndef UDE_ROWS16
+#define UDE_ROWS16 1
+#endif
 #ifndef UDE_FWD_EARLY_ST
-#define UDE_FWD_EARLY_ST 1
+#define UDE_FWD_EARLY_ST 0
 #endif
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
@@ -488,6 +493,71 @@ __device__ __forceinline__ void load_static(const float* __restrict__ y0, float*
   }
 }
 
+// Forward tile start, the y0 traffic besides the stage input (L = 8, 16-B aligned y0 / latent): the
+// record's static features and -- LATENT -- latent[0] and the static latent dims of every output time
+// (zero derivative, carried unchanged: lib/models.py:144).  Row-mapped (consecutive lanes, consecutive
+// 32-B (n, r) rows of the tile's contiguous (16, R, 8) block) and every load issued before the first
+// store: loads and stores count together in vmcnt, so a load issued behind pending stores waits for
+// them to complete (the per-output copy loop this replaces waited once per iteration: ~18% of the
+// state49 training forward in tools/stage_profile.py).
+template <class M, int SR, int XOFF, bool LATENT>
+__device__ __forceinline__ void fwd_tile_io(const KArgs& A, const Sched& sc, float* lds, int n0) {
+  static_assert(M::L == 8, "row-mapped tile start: L = 8");
+  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS;
+  constexpr int PS = (TT * M::S16 + NTHREADS - 1) / NTHREADS, CS = 4;
+  int tid = threadIdx.x;
+  // the thread-derived offsets are formed here each tile, not hoisted out of the tile loop into
+  // registers the stage loop needs
+  asm volatile("" : "+v"(tid));
+  const int nvalid = min(TT, A.n_traj - n0) * M::R;
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  // the record's static features, CS loads in flight at a time (no global store is pending yet)
+#pragma unroll
+  for (int u0 = 0; u0 < PS; u0 += CS) {
+    float sv[CS];
+#pragma unroll
+    for (int uu = 0; uu < CS; ++uu) {
+      const int i = tid + (u0 + uu) * NTHREADS;
+      const int t = i / M::S16, s = i - t * M::S16;
+      const int n = n0 + t;
+      float v = 0.f;
+      if (u0 + uu < PS && i < TT * M::S16 && s < M::S && n < A.n_traj) {
+        const int r = s / (M::L - 3), c = 3 + s - r * (M::L - 3);
+        v = A.y0[((size_t)n * M::R + r) * M::L + c];
+      }
+      sv[uu] = v;
+    }
+#pragma unroll
+    for (int uu = 0; uu < CS; ++uu) {
+      const int i = tid + (u0 + uu) * NTHREADS;
+      const int t = i / M::S16, s = i - t * M::S16;
+      if (u0 + uu < PS && i < TT * M::S16) lds[t * SR + XOFF + s] = sv[uu];
+    }
+  }
+  if constexpr (LATENT) {
+    // latent[0] and the static dims of every output, one row per lane at a time (one wait per row
+    // slot; holding every slot's row across the output loop spilled registers of the stage loop)
+    #pragma unroll 1
+    for (int u = 0; u < PR; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < nvalid) {
+        const size_t row = ((size_t)n0 * M::R + i) * M::L;
+        const f4* src = reinterpret_cast<const f4*>(A.y0 + row);
+        const f4 lo = src[0], hi = src[1];
+        f4* d0 = reinterpret_cast<f4*>(A.latent + row);
+        d0[0] = lo;
+        d0[1] = hi;
+        #pragma unroll 1
+        for (int o = 0; o < A.n_out; ++o) {
+          float* d = A.latent + (size_t)sc.out_j[o] * NRL + row;
+          d[3] = lo[3];
+          *reinterpret_cast<f4*>(d + 4) = hi;
+        }
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, int stage, int F, int f, int t) {
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
@@ -630,6 +700,8 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
       }
     };
 
+    // the row-mapped tile start (fwd_tile_io; L = 8: y0 / latent 16-B aligned, checked by the host entry)
+    constexpr bool rows16 = UDE_ROWS16 && M::L == 8;
     // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
     sfor<SL>([&](auto ss) {
       constexpr int sl = decltype(ss)::value;
@@ -646,15 +718,16 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
           if (TRAIN && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
           if (DEC && valid) *st_reg += (double)reg_term(ys[sl][c]);
         }
-        if (valid && !DEC) {
+        if (valid && !DEC && !rows16) {
           float* dst = A.latent + ((size_t)n * M::R + r) * M::L;
           for (int c = 0; c < M::L; ++c) dst[c] = src[c];
         }
       }
     });
+    if constexpr (rows16) fwd_tile_io<M, SR, M::XSF_OFF, !DEC>(A, sc, lds, n0);
     // static latent dims (zero derivative, carried unchanged: lib/models.py:144) of every output
     // time, once per tile (not in the step loop, where each copy waited on a global load)
-    if constexpr (M::L > 3 && !DEC) {
+    if constexpr (M::L > 3 && !DEC && !rows16) {
       #pragma unroll 1
       for (int i = tid; i < A.n_out * M::PAIRS; i += NTHREADS) {
         const int o = i / M::PAIRS, p = i - o * M::PAIRS;
@@ -667,7 +740,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         }
       }
     }
-    load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
+    if constexpr (!rows16) load_static<M, SR, M::XSF_OFF>(A.y0, lds, n0, A.n_traj);
     lds_sync();
     if constexpr (TRAIN && M::GST) {
       // the tile's static features once ([tile][16][S16] behind the stored rows): the weight-gradient

@@ -145,16 +145,17 @@ def test_bayes_state49_full_batch(pkg):
     assert K >= N - 64 and int(far.sum()) >= 1000, (K, int(far.sum()))
     # rows: the latent of every agreeing trajectory (1e-6); dy0 of those that keep 1e-3 away from the mask
     # boundary (next to it fp32 rounding alone moves the gradient, test_north_star) and whose rates keep
-    # away from the kink of |.| (a sign flip of d|h|/dh there): 4e-5 between the two fp32 paths, each held
-    # to 2e-5 of fp64 (the whole-solve one on the 256 trajectories above)
-    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 4e-5, rows
+    # away from the kink of |.| (a sign flip of d|h|/dh there; with the 114 such trajectories of this batch
+    # in the set the two paths' dy0 differed by 3.7e-5 and their d mean / d std sums by 4e-4 / 8e-4,
+    # without them 3e-7 and 1.1e-6): 5e-6 between the two fp32 paths
+    assert rows["latent"] <= 1e-6 and rows["y0_far"] <= 5e-6, rows
     # the batch sums (posterior, |Fa|, every d mean / d std) over the trajectories that keep away from it
     fused, per, errs, agree2, _, _ = _bayes_pair(pkg, mod, y0[far].contiguous(), t, h, eps, dl[:, far].contiguous())
     print(f"  the {int(far.sum())} as one batch: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     assert bool(agree2.all())
     for k in ("latent", "mean", "std", "fa_norm"):
         assert errs[k] <= 1e-6, (k, errs[k])
-    assert errs["y0"] <= 4e-5 and errs["d_mean"] <= 5e-5 and errs["d_std"] <= 5e-5, errs
+    assert errs["y0"] <= 5e-6 and errs["d_mean"] <= 1e-5 and errs["d_std"] <= 1e-5, errs
 
 
 @pytest.mark.timeout(1200)

@@ -27,7 +27,7 @@ def one(ic):
     i, c = ic
     d = os.path.join(tmp, str(i))
     os.makedirs(d)
-    cmd = [_native.HIPCC, *_native.HIP_FLAGS, "--offload-device-only", "-S", "-I", _native.INCLUDE, "-I",
+    cmd = [_native.HIPCC, *_native.HIP_FLAGS, *os.environ.get("SPILL_FLAGS", "").split(), "--offload-device-only", "-S", "-I", _native.INCLUDE, "-I",
            _native.CSRC, "-I", gen, os.path.join(_native.CSRC, "ude_cfg.hip"), f"-DUDE_CFG_ID={i}",
            f"-DUDE_ONE_CONFIG={configs.template_args(c)}", "-o", os.path.join(d, "k.s")]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -215,7 +215,6 @@ struct Ops {
     }
     if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !stats_out || !reg_out)
       return UDE_E_INVALID;
-    if (M::L == 8 && (reinterpret_cast<uintptr_t>(y0) & 15)) return UDE_E_INVALID;   // 16-B y0 rows
     if (p->n_steps < 1) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -371,8 +370,8 @@ struct Ops {
                                                                   stats_out, s);
     }
     if (!pack || !sched || !y0 || !latent || !stats_slab || !stats_out) return UDE_E_INVALID;
-    if (M::L == 8 && ((reinterpret_cast<uintptr_t>(y0) | reinterpret_cast<uintptr_t>(latent)) & 15))
-      return UDE_E_INVALID;                          // the row-mapped tile start reads / writes 16-B rows
+    if (M::L == 8 && (reinterpret_cast<uintptr_t>(latent) & 15))
+      return UDE_E_INVALID;                          // the row-mapped tile start writes 16-B latent rows
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     const int n_tiles = (p->n_traj + TT - 1) / TT;

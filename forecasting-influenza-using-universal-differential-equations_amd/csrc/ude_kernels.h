@@ -493,25 +493,15 @@ __device__ __forceinline__ void load_static(const float* __restrict__ y0, float*
   }
 }
 
-// Forward tile start, the y0 traffic besides the stage input (L = 8, 16-B aligned y0 / latent): the
-// record's static features and -- LATENT -- latent[0] and the static latent dims of every output time
-// (zero derivative, carried unchanged: lib/models.py:144).  Row-mapped (consecutive lanes, consecutive
-// 32-B (n, r) rows of the tile's contiguous (16, R, 8) block) and every load issued before the first
-// store: loads and stores count together in vmcnt, so a load issued behind pending stores waits for
-// them to complete (the per-output copy loop this replaces waited once per iteration: ~18% of the
-// state49 training forward in tools/stage_profile.py).
-template <class M, int SR, int XOFF, bool LATENT>
-__device__ __forceinline__ void fwd_tile_io(const KArgs& A, const Sched& sc, float* lds, int n0) {
-  static_assert(M::L == 8, "row-mapped tile start: L = 8");
-  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS;
+// Forward tile start (L = 8), before the stage input: the record's static features from y0, CS loads in
+// flight at a time, ahead of any global store of the tile (loads and stores count together in vmcnt, so a
+// load issued behind pending stores waits for them to complete).
+template <class M, int SR, int XOFF>
+__device__ __forceinline__ void fwd_tile_static(const KArgs& A, float* lds, int n0) {
   constexpr int PS = (TT * M::S16 + NTHREADS - 1) / NTHREADS, CS = 4;
   int tid = threadIdx.x;
-  // the thread-derived offsets are formed here each tile, not hoisted out of the tile loop into
-  // registers the stage loop needs
+  // thread-derived offsets formed here each tile, not hoisted into registers the stage loop needs
   asm volatile("" : "+v"(tid));
-  const int nvalid = min(TT, A.n_traj - n0) * M::R;
-  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
-  // the record's static features, CS loads in flight at a time (no global store is pending yet)
 #pragma unroll
   for (int u0 = 0; u0 < PS; u0 += CS) {
     float sv[CS];
@@ -534,25 +524,37 @@ __device__ __forceinline__ void fwd_tile_io(const KArgs& A, const Sched& sc, flo
       if (u0 + uu < PS && i < TT * M::S16) lds[t * SR + XOFF + s] = sv[uu];
     }
   }
-  if constexpr (LATENT) {
-    // latent[0] and the static dims of every output, one row per lane at a time (one wait per row
-    // slot; holding every slot's row across the output loop spilled registers of the stage loop)
-    #pragma unroll 1
-    for (int u = 0; u < PR; ++u) {
-      const int i = tid + u * NTHREADS;
-      if (i < nvalid) {
-        const size_t row = ((size_t)n0 * M::R + i) * M::L;
-        const f4* src = reinterpret_cast<const f4*>(A.y0 + row);
-        const f4 lo = src[0], hi = src[1];
-        f4* d0 = reinterpret_cast<f4*>(A.latent + row);
-        d0[0] = lo;
-        d0[1] = hi;
-        #pragma unroll 1
-        for (int o = 0; o < A.n_out; ++o) {
-          float* d = A.latent + (size_t)sc.out_j[o] * NRL + row;
-          d[3] = lo[3];
-          *reinterpret_cast<f4*>(d + 4) = hi;
-        }
+}
+
+// latent[0] and the static latent dims of every output time (zero derivative, carried unchanged:
+// lib/models.py:144), from the record (stage input in the Y slot, static features at XOFF) after the
+// tile-start barrier: stores only, row-mapped (consecutive lanes, consecutive 32-B (n, r) rows of the
+// tile's contiguous (16, R, 8) latent block).  The per-output copy loop this replaces read y0 once per
+// iteration behind its own pending stores (18% of the state49 training forward, tools/stage_profile.py).
+template <class M, int SR, int XOFF>
+__device__ __forceinline__ void fwd_tile_latent(const KArgs& A, const Sched& sc, const float* lds, int n0) {
+  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int nvalid = min(TT, A.n_traj - n0) * M::R;
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  #pragma unroll 1
+  for (int u = 0; u < PR; ++u) {
+    const int i = tid + u * NTHREADS;
+    if (i < nvalid) {
+      const int t = i / M::R, r = i - t * M::R;
+      const float* rec = lds + t * SR;
+      const f4 lo = {rec[M::Y_OFF + 3 * r], rec[M::Y_OFF + 3 * r + 1], rec[M::Y_OFF + 3 * r + 2], rec[XOFF + 5 * r]};
+      const f4 hi = {rec[XOFF + 5 * r + 1], rec[XOFF + 5 * r + 2], rec[XOFF + 5 * r + 3], rec[XOFF + 5 * r + 4]};
+      const size_t row = ((size_t)n0 * M::R + i) * M::L;
+      f4* d0 = reinterpret_cast<f4*>(A.latent + row);
+      d0[0] = lo;
+      d0[1] = hi;
+      #pragma unroll 1
+      for (int o = 0; o < A.n_out; ++o) {
+        float* d = A.latent + (size_t)sc.out_j[o] * NRL + row;
+        d[3] = lo[3];
+        *reinterpret_cast<f4*>(d + 4) = hi;
       }
     }
   }
@@ -700,8 +702,10 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
       }
     };
 
-    // the row-mapped tile start (fwd_tile_io; L = 8: y0 / latent 16-B aligned, checked by the host entry)
+    // the row-mapped tile start (fwd_tile_static / fwd_tile_latent; L = 8: 16-B latent rows, checked by
+    // the host entry)
     constexpr bool rows16 = UDE_ROWS16 && M::L == 8;
+    if constexpr (rows16) fwd_tile_static<M, SR, M::XSF_OFF>(A, lds, n0);
     // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
     sfor<SL>([&](auto ss) {
       constexpr int sl = decltype(ss)::value;
@@ -724,7 +728,6 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         }
       }
     });
-    if constexpr (rows16) fwd_tile_io<M, SR, M::XSF_OFF, !DEC>(A, sc, lds, n0);
     // static latent dims (zero derivative, carried unchanged: lib/models.py:144) of every output
     // time, once per tile (not in the step loop, where each copy waited on a global load)
     if constexpr (M::L > 3 && !DEC && !rows16) {
@@ -755,7 +758,8 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     }
     f4 c1[M::NZ(W) > 0 ? M::NZ(W) : 1];
     static_hoist<M, W, SR, M::XSF_OFF>(rs, lds, c1, lane);
-    lds_sync();
+    if constexpr (rows16 && !DEC) fwd_tile_latent<M, SR, M::XSF_OFF>(A, sc, lds, n0);
+    lds_sync();                                   // the static features (aliased by the activations) are dead
     if constexpr (DEC) dec_emit(0);               // output 0 = y0
     UDE_STAMP(pf, 15);
 

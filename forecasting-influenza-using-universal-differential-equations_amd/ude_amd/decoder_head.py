@@ -78,12 +78,12 @@ def solve_decode(ode, y0: torch.Tensor, t: torch.Tensor, step_size, linear: torc
         mus, sds = ode.ude_mean_std()
         eps = ode.take_eps(4 * plan.prob.n_steps, sum(int(p.numel()) for p in mus), y0.device)
         yhat, reg, stats, token, ckpt, sums = _fused.FusedBayesRK4Dec.apply(
-            plan, _fused.aligned_y0(y0), eps, linear.weight, linear.bias, *(mus + sds))
+            plan, y0.contiguous(), eps, linear.weight, linear.bias, *(mus + sds))
     else:
         params = []
         for lin in ode.ude_linears():
             params += [lin.weight, lin.bias]
-        yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, _fused.aligned_y0(y0), linear.weight,
+        yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight,
                                                                       linear.bias, *params)
     ode._record_fused(stats, plan.n_eval, sums=sums)
     return yhat, reg, LazyLatent(token, ckpt, y0, plan), plan

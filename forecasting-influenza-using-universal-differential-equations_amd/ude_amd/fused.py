@@ -120,13 +120,6 @@ def _is_placeholder(g: torch.Tensor) -> bool:
     return z is not None and g.data_ptr() == z.data_ptr() and all(st == 0 for st in g.stride())
 
 
-def aligned_y0(y0: torch.Tensor) -> torch.Tensor:
-    """y0 as the forward kernels read it: contiguous, its (n, r) rows 16-B aligned (the L = 8 tile start
-    moves whole 32-B rows; a contiguous view at another offset is copied once)."""
-    y0 = y0.contiguous()
-    return y0 if y0.data_ptr() % 16 == 0 else y0.clone()
-
-
 def sir_token_like(latent: torch.Tensor) -> torch.Tensor:
     """Stride-0 (T, N, R, 3) placeholder output of a fused solve: a consumer that reads only
     latent[..., :3] (the fused loss head) takes it as an input and returns its compact S, I, R

@@ -107,7 +107,21 @@ __device__ __forceinline__ float reg_term(float v) {
 // HBM during the next layer's phase, issued behind that phase's weight loads.  Off: measured slower
 // (profiles/r04/ab_early_*.log: state49 fwd 1.075 vs 1.041 ms, Bayes state49 1.835 vs 1.742 ms) --
 // the stores then compete with the phases' weight and operand traffic instead of the flux pass
-// the forward's row-mapped tile start (fwd_tile_io); -DUDE_ROWS16=0: the per-pair copy loops (A/B)
+// large records (R > ~20): the training forward writes each stage's checkpointed input from the
+// record's Y slot as 16-B stores along the trajectories, behind phase 0's weight loads (state49 fwd
+// 0.945 -> 0.925 ms; at R = 1 it cost M1 2%: small records keep three 4-B stores per (trajectory,
+// region) in the flux pass; -DUDE_CKPT_ROWS=0 everywhere, profiles/r04/ab_ck_*.log)
+#ifndef UDE_CKPT_ROWS
+#define UDE_CKPT_ROWS 1
+#endif
+// -DUDE_LAT_ROWS=1: the latent's grid-hit outputs (schedule mode 1) written row-mapped from the
+// record's Y slot during the next step's first layer phase instead of pair-mapped by the flux pass.
+// Off: no gain at state49 (0.925 vs 0.928 ms), 0.2% slower at M1 (profiles/r04/ab_ck_*.log)
+#ifndef UDE_LAT_ROWS
+#define UDE_LAT_ROWS 0
+#endif
+// the forward's row-mapped tile start (fwd_tile_static / fwd_tile_latent); -DUDE_ROWS16=0: the per-pair
+// copy loops (A/B)
 #ifndef UDE_ROWS16
 #define UDE_ROWS16 1
 #endif
@@ -564,6 +578,56 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
 
+// The grid-hit outputs (mode 1) of RK step `step` -- y_{step+1}, the record's Y slot from the flux
+// barrier of the step's last stage until the next one -- row-mapped: consecutive lanes write the S, I, R
+// of consecutive (n, r) rows of the tile's contiguous (16, R, L) block (the flux pass's pair mapping
+// put consecutive lanes R * L floats apart).
+template <class M, int SR>
+__device__ __forceinline__ void store_latent_rows(const KArgs& A, const Sched& sc, const float* lds, int n0,
+                                                  int step, int tid) {
+  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS;
+  asm volatile("" : "+v"(tid));
+  const int nvalid = min(TT, A.n_traj - n0) * M::R;
+  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
+  const int o_end = sc.out_start[step + 1];
+  #pragma unroll 1
+  for (int o = sc.out_start[step]; o < o_end; ++o) {
+    if (sc.out_mode[o] != 1) continue;
+    float* base = A.latent + (size_t)sc.out_j[o] * NRL + (size_t)n0 * M::R * M::L;
+#pragma unroll
+    for (int u = 0; u < PR; ++u) {
+      const int i = tid + u * NTHREADS;
+      if (i < nvalid) {
+        const int t = i / M::R, r = i - t * M::R;
+        const float* y = lds + t * SR + M::Y_OFF + 3 * r;
+        float* d = base + (size_t)i * M::L;
+        d[0] = y[0];
+        d[1] = y[1];
+        d[2] = y[2];
+      }
+    }
+  }
+}
+
+// The stage input in the record's Y slot ([16][F] at Y_OFF) -> its checkpoint block ([F][16]): lane
+// (f, q) gathers trajectories 4q .. 4q + 3 of feature f (conflict-free LDS reads: consecutive lanes,
+// consecutive banks) and writes them as one 16-B store; 64 lanes cover 1 KB of the block.
+template <class M, int SR>
+__device__ __forceinline__ void store_ckpt_rows(float* blk, const float* lds, int tid) {
+  constexpr int NQ = M::F * (TT / 4), PER = (NQ + NTHREADS - 1) / NTHREADS;
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + u * NTHREADS;
+    if (i < NQ) {
+      const int f = i >> 2, t0 = (i & 3) * 4;
+      const f4 v = {lds[t0 * SR + M::Y_OFF + f], lds[(t0 + 1) * SR + M::Y_OFF + f],
+                    lds[(t0 + 2) * SR + M::Y_OFF + f], lds[(t0 + 3) * SR + M::Y_OFF + f]};
+      reinterpret_cast<f4*>(blk)[i] = v;
+    }
+  }
+}
+
 // GST training forward: the tiles' static features ([tile][16][S16]) behind the stage checkpoints and
 // stored rows (the weight-gradient GEMM's layer-0 input beside each stage's stored input).
 template <class M>
@@ -705,6 +769,8 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
     // the row-mapped tile start (fwd_tile_static / fwd_tile_latent; L = 8: 16-B latent rows, checked by
     // the host entry)
     constexpr bool rows16 = UDE_ROWS16 && M::L == 8;
+    constexpr bool LAT_ROWS = UDE_LAT_ROWS && !DEC;
+    constexpr bool CKR = UDE_CKPT_ROWS && SL > 1;           // large records: checkpoint rows
     if constexpr (rows16) fwd_tile_static<M, SR, M::XSF_OFF>(A, lds, n0);
     // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
     sfor<SL>([&](auto ss) {
@@ -719,7 +785,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         for (int c = 0; c < 3; ++c) {
           ys[sl][c] = valid ? src[c] : 0.f;
           lds[t * SR + M::Y_OFF + 3 * r + c] = ys[sl][c];
-          if (TRAIN && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
+          if (TRAIN && !CKR && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
           if (DEC && valid) *st_reg += (double)reg_term(ys[sl][c]);
         }
         if (valid && !DEC && !rows16) {
@@ -784,10 +850,24 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
           mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
             constexpr int d = decltype(dd)::value;
             if constexpr (d >= 1) store_act_layer<M, SR, d - 1>(blk, lds, tid);
+            if constexpr (d == 0 && CKR)
+              store_ckpt_rows<M, SR>(A.ckpt + ckpt_index(tile, A.n_steps, step, j, M::F, 0, 0), lds, tid);
           });
           store_act_layer<M, SR, M::D - 1>(blk, lds, tid);
         } else {
-          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf);
+          // this stage's input (the record's Y slot, layer 0's input) -> its checkpoint, issued behind
+          // phase 0's weight loads (their waits then do not wait for these stores) and read before
+          // the phase's barrier (the flux pass overwrites the slot after the last phase)
+          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
+            if constexpr (decltype(dd)::value == 0) {
+              if constexpr (TRAIN && CKR)
+                store_ckpt_rows<M, SR>(A.ckpt + ckpt_index(tile, A.n_steps, step, j, M::F, 0, 0), lds, tid);
+              // the previous step's grid-hit outputs (y_step, this stage's input)
+              if constexpr (LAT_ROWS) {
+                if (j == 0 && step > 0) store_latent_rows<M, SR>(A, sc, lds, n0, step - 1, tid);
+              }
+            }
+          });
         }
         if constexpr (PFB) {
           const int en = 4 * step + j + 1;
@@ -840,7 +920,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
               const float plus = (b * Y[0]) * Y[1];
               const float minus = gm * Y[1];
               f[0] = -plus; f[1] = plus - minus; f[2] = minus;
-              if (valid) {
+              if (valid && UDE_ABL != 14) {
                 st_b += (double)b; st_g += (double)gm;
                 st_bb += (double)b * (double)b; st_gg += (double)gm * (double)gm;
               }
@@ -851,7 +931,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
                 const float fa = rec[M::act_off(1, M::nl(1) - 1) + 3 * r + c];
                 if constexpr (M::HAS_P) f[c] = f[c] + A.fa_w * fa;
                 else f[c] = fa;
-                if (valid) st_fa += (double)fa * (double)fa;
+                if (valid && UDE_ABL != 14) st_fa += (double)fa * (double)fa;
               }
             }
 #pragma unroll
@@ -886,11 +966,12 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 #pragma unroll
                   for (int c = 0; c < 3; ++c) A.ckpt_final[((size_t)tile * M::F + 3 * r + c) * TT + t] = ys[sl][c];
                 }
-              } else if (valid) {
+              } else if (valid && UDE_ABL != 16) {
                 const int o_end = sc.out_start[step + 1];
                 #pragma unroll 1
                 for (int o = sc.out_start[step]; o < o_end; ++o) {
                   const int jo = sc.out_j[o], mode = sc.out_mode[o];
+                  if (LAT_ROWS && mode == 1) continue;       // store_latent_rows, next step
                   const float slope = sc.out_slope[o];
                   float* dst = A.latent + (size_t)jo * NRL + ((size_t)n * M::R + r) * M::L;
 #pragma unroll
@@ -909,7 +990,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
             if (TRAIN) {
               const int ns = j == 3 ? step + 1 : step;
               const int nj = j == 3 ? 0 : j + 1;
-              if (ns < A.n_steps) {
+              if (!CKR && ns < A.n_steps && UDE_ABL != 15) {
 #pragma unroll
                 for (int c = 0; c < 3; ++c)
                   A.ckpt[ckpt_index(tile, A.n_steps, ns, nj, M::F, 3 * r + c, t)] = Yn[c];
@@ -924,6 +1005,12 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
       if constexpr (DEC) {
         if (sc.out_start[step] < sc.out_start[step + 1]) dec_emit(sc.out_j[sc.out_start[step]]);
       }
+    }
+    if constexpr (LAT_ROWS) {
+      // the last step's grid-hit outputs; the next tile's stage input overwrites the Y slot after
+      // this barrier
+      if (A.n_steps > 0) store_latent_rows<M, SR>(A, sc, lds, n0, A.n_steps - 1, tid);
+      lds_sync();
     }
   }
 
@@ -952,7 +1039,7 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 // Training forward of small records (Model::split_fwd): waves 4-7 store each stage's activation
 // rows (the backward's input) from the record to HBM while waves 0-3 run the flux pass; the same
 // barrier sequence as fwd_body.
-template <class M>
+template <class M, bool DEC>
 __device__ void fwd_sbody(const KArgs& A, float* lds) {
   constexpr int SR = M::SR_F;
   constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
@@ -983,6 +1070,7 @@ __device__ void fwd_sbody(const KArgs& A, float* lds) {
         lds_sync();                            // flux pass (the next stage rewrites the rows)
       }
     }
+    if constexpr (UDE_LAT_ROWS && !DEC) lds_sync();   // the last step's latent rows
   }
   lds_sync();                                  // side-statistic reduction
   lds_sync();
@@ -995,7 +1083,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * NTHREADS : NTHREADS, (SPLIT || RES) ? 1
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (SPLIT) {
-    if (w >= WAVES) { fwd_sbody<M>(a, lds); return; }
+    if (w >= WAVES) { fwd_sbody<M, DEC>(a, lds); return; }
   }
   if (w == 0) fwd_body<M, TRAIN, 0, SPLIT, DEC, RES>(a, lds);
   else if (w == 1) fwd_body<M, TRAIN, 1, SPLIT, DEC, RES>(a, lds);

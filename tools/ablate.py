@@ -7,7 +7,9 @@ GPU box, each library is timed on the bench's M1 backward and the per-variant ke
   4 no stage-input copy  5 no layer-0 sum / RK adjoint  6 no phase-1 weight gradients
   7 no input-gradient phases
   large records (ABL_WORKLOAD=state49): 21 no partner dW MFMAs  22 no activation-row LDS-DMA
-  8 no stage-start activation load (4-wave large path)  12 / 11 / 13 forward ablations
+  8 no stage-start activation load (4-wave large path)  12 / 11 / 13 forward ablations (no flux pass /
+  no activation-row stores / no layer MFMAs)  14 / 15 / 16 forward flux pass: no fp64 side sums / no
+  stage-input checkpoint stores / no latent output stores
 """
 import importlib
 import os

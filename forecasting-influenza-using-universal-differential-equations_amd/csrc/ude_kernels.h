@@ -107,6 +107,12 @@ __device__ __forceinline__ float reg_term(float v) {
 // HBM during the next layer's phase, issued behind that phase's weight loads.  Off: measured slower
 // (profiles/r04/ab_early_*.log: state49 fwd 1.075 vs 1.041 ms, Bayes state49 1.835 vs 1.742 ms) --
 // the stores then compete with the phases' weight and operand traffic instead of the flux pass
+// split backward kernels, -DUDE_PRIO=1: the critical-path waves run at a raised issue priority
+// (s_setprio 2).  Off: no gain (profiles/r04/ab_prio_*.log: state49 bwd 1.833 vs 1.806 ms, M1 and
+// M1 Fp [32,32] within 0.3%)
+#ifndef UDE_PRIO
+#define UDE_PRIO 0
+#endif
 // large records (R > ~20): the training forward writes each stage's checkpointed input from the
 // record's Y slot as 16-B stores along the trajectories, behind phase 0's weight loads (state49 fwd
 // 0.945 -> 0.925 ms; at R = 1 it cost M1 2%: small records keep three 4-B stores per (trajectory,
@@ -2609,6 +2615,9 @@ __global__ __launch_bounds__(M::BWD_THREADS) void ude_bwd_kernel(KArgs a) {
       return;
     }
   }
+  // UDE_PRIO: the critical-path waves win the issue arbitration against their partner waves on the
+  // same SIMD (tried because either stream alone takes 1.45 ms, both 1.94: profiles/r04/abl3_state49_bwd.log)
+  if constexpr ((M::SPLIT_BWD || M::SPLIT_BWD_L) && UDE_PRIO) __builtin_amdgcn_s_setprio(2);
   if (w == 0) bwd_body<M, 0>(a, lds);
   else if (w == 1) bwd_body<M, 1>(a, lds);
   else if (w == 2) bwd_body<M, 2>(a, lds);

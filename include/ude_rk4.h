@@ -132,7 +132,9 @@ int ude_pack_weights_bayes(const UdeModelDesc* m, const UdeProblem* p, const flo
  * (entries of an absent net are 0); on return stats_slab[0..4] holds the fp64
  * totals {sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2} those are
  * formed from (the data-parallel statistics exchange all-reduces them; the
- * same holds for ude_rk4_forward_dec and ude_dopri5_forward's workspace). */
+ * same holds for ude_rk4_forward_dec and ude_dopri5_forward's workspace).
+ * With L = 8, latent must be 16-byte aligned (the tile start writes its 32-B
+ * (n, r) rows with 16-B stores): UDE_E_INVALID otherwise. */
 int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pack,
                     const void* sched, const float* y0, float* latent, float* ckpt,
                     double* stats_slab, float* stats_out, ude_stream_t stream);

@@ -124,6 +124,17 @@ struct Ops {
   static hipError_t static_tsum(const UdeProblem* p, const float* dlatent, float* dy0, hipStream_t s) {
     if constexpr (M::FULL0) {
       if (dlatent) {
+        if constexpr (M::L == 8) {
+          if (((reinterpret_cast<uintptr_t>(dlatent) | reinterpret_cast<uintptr_t>(dy0)) & 15) == 0) {
+            const long rows = (long)p->n_traj * M::R;
+            long blocks = (rows + 255) / 256;
+            if (blocks > 8192) blocks = 8192;
+            if (blocks < 1) blocks = 1;
+            hipLaunchKernelGGL((ude_static_tsum_rows_kernel<M>), dim3((unsigned)blocks), dim3(256), 0, s, dlatent,
+                               p->n_traj, p->n_out + 1, dy0);
+            return hipGetLastError();
+          }
+        }
         const long total = (long)p->n_traj * M::R * (M::L - 3);
         long blocks = (total + 255) / 256;
         if (blocks > 4096) blocks = 4096;

@@ -2258,6 +2258,30 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
 #endif
 }
+// L = 8, 16-B aligned rows: one thread per (n, r) row, whole 32-B rows loaded (both 16-B halves of every
+// output time in flight at once, coalesced), the same additions in the same order as the scalar kernel
+// below (dy0 first, then output times ascending): bitwise the same dy0.
+template <class M>
+__global__ __launch_bounds__(256) void ude_static_tsum_rows_kernel(const float* __restrict__ dlatent, int n_traj,
+                                                                   int n_times, float* __restrict__ dy0) {
+  static_assert(M::L == 8, "row kernel: L = 8");
+  const size_t NR = (size_t)n_traj * M::R, NRL = NR * M::L;
+  for (size_t nr = (size_t)blockIdx.x * 256 + threadIdx.x; nr < NR; nr += (size_t)gridDim.x * 256) {
+    f4* d = reinterpret_cast<f4*>(dy0 + nr * M::L);
+    f4 lo = d[0], hi = d[1];
+    float v3 = lo[3];
+    #pragma unroll 3
+    for (int jt = 0; jt < n_times; ++jt) {
+      const f4* g = reinterpret_cast<const f4*>(dlatent + (size_t)jt * NRL + nr * M::L);
+      v3 += g[0][3];
+      hi += g[1];
+    }
+    lo[3] = v3;
+    d[0] = lo;
+    d[1] = hi;
+  }
+}
+
 // FULL0 (Bayesian RHS, static dims in the solve's layer 0): dy0[n, r, c >= 3] += sum_j dlatent[j, n, r, c]
 // in output order j (the same additions as one loop after the input-gradient sum).
 template <class M>

@@ -120,6 +120,12 @@ def _is_placeholder(g: torch.Tensor) -> bool:
     return z is not None and g.data_ptr() == z.data_ptr() and all(st == 0 for st in g.stride())
 
 
+def _d_std(d_abs: torch.Tensor, sds) -> torch.Tensor:
+    """d/d std from the kernel's flat d/d |std| (torch's abs backward: times sign(std)) for every std
+    tensor at once -- three device operators instead of two per tensor."""
+    return d_abs * torch.sign(torch.cat([s.reshape(-1) for s in sds]))
+
+
 def sir_token_like(latent: torch.Tensor) -> torch.Tensor:
     """Stride-0 (T, N, R, 3) placeholder output of a fused solve: a consumer that reads only
     latent[..., :3] (the fused loss head) takes it as an input and returns its compact S, I, R
@@ -271,8 +277,7 @@ class FusedBayesRK4Dec(torch.autograd.Function):
         dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent)
         n = plan.sizes.n_params // 2
         d_mu = _split(dparams[:n], plan.param_shapes)
-        d_abs = _split(dparams[n:], plan.param_shapes)
-        d_sd = [g * torch.sign(s) for g, s in zip(d_abs, sds)]
+        d_sd = _split(_d_std(dparams[n:], sds), plan.param_shapes)
         return (None, dy0, None, dWd, dbd) + tuple(d_mu) + tuple(d_sd)
 
 
@@ -480,6 +485,5 @@ class FusedBayesRK4(torch.autograd.Function):
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         n = plan.sizes.n_params // 2
         d_mu = _split(dparams[:n], plan.param_shapes)
-        d_abs = _split(dparams[n:], plan.param_shapes)
-        d_sd = [g * torch.sign(s) for g, s in zip(d_abs, sds)]
+        d_sd = _split(_d_std(dparams[n:], sds), plan.param_shapes)
         return (None, dy0, None, None) + tuple(d_mu) + tuple(d_sd)

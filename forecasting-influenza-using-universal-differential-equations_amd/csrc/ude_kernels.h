@@ -107,9 +107,11 @@ __device__ __forceinline__ float reg_term(float v) {
 // HBM during the next layer's phase, issued behind that phase's weight loads.  Off: measured slower
 // (profiles/r04/ab_early_*.log: state49 fwd 1.075 vs 1.041 ms, Bayes state49 1.835 vs 1.742 ms) --
 // the stores then compete with the phases' weight and operand traffic instead of the flux pass
-// training forward (large records): activation-row quads per LDS-read / store batch of the tail copy
+// training forward (large records): activation-row quads per LDS-read / store batch of the tail copy.
+// All of them at once (state49 fwd 0.936 -> 0.892 ms against batches of 3, profiles/r04/ab_uc_*.log;
+// the tail runs after the layer phases, whose registers are free by then)
 #ifndef UDE_TAIL_UC
-#define UDE_TAIL_UC 3
+#define UDE_TAIL_UC 16
 #endif
 // split backward kernels, -DUDE_PRIO=1: the critical-path waves run at a raised issue priority
 // (s_setprio 2).  Off: no gain (profiles/r04/ab_prio_*.log: state49 bwd 1.833 vs 1.806 ms, M1 and
@@ -888,8 +890,8 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
           constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
-          // in chunks of UC quads (the forward runs two workgroups per CU: 256 registers)
-          constexpr int UC = NQ <= 5 ? NQ : UDE_TAIL_UC;
+          // UC quads per batch (UDE_TAIL_UC; the forward runs two workgroups per CU: 256 registers)
+          constexpr int UC = NQ <= 5 ? NQ : cmin(NQ, UDE_TAIL_UC);
           #pragma unroll 1
           for (int u0 = 0; u0 < NQ; u0 += UC) {
 #pragma unroll

@@ -2937,29 +2937,22 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
   const int tile = blockIdx.x;
   const size_t NRL = (size_t)n_traj * M::R * M::L;
-  // (1) the time sums of the tile's d latent block (HBM stream) into LDS
-  auto time_sums = [&]() {
-    if (!dlatent) {                                  // static cotangents all zero
-      #pragma unroll 1
-      for (int i = threadIdx.x; i < BLK; i += 256) tsum[i] = 0.f;
-      return;
-    }
+  if (!dlatent) {                                    // static cotangents all zero
+    #pragma unroll 1
+    for (int i = threadIdx.x; i < BLK; i += 256) tsum[i] = 0.f;
+  } else {
     const int nvalid = min(TT, n_traj - tile * TT) * M::R * M::L;
     const float* blk = dlatent + (size_t)tile * BLK;
     if constexpr ((M::R * M::L) % 4 == 0) {
-      // 16-B loads, two positions x every output time in flight per lane (each sum stays in time order)
+      // 16-B loads, 8 output times in flight per lane (the sums stay in time order)
       #pragma unroll 1
-      for (int i = 4 * threadIdx.x; i < BLK; i += 8 * 256) {
-        const int i2 = i + 4 * 256;
-        f4 v = f4zero(), v2 = f4zero();
-        const bool ok = i < nvalid, ok2 = i2 < nvalid;
-#pragma unroll 9
-        for (int jt = 0; jt < n_times; ++jt) {
-          if (ok) v += *reinterpret_cast<const f4*>(blk + (size_t)jt * NRL + i);
-          if (ok2) v2 += *reinterpret_cast<const f4*>(blk + (size_t)jt * NRL + i2);
+      for (int i = 4 * threadIdx.x; i < BLK; i += 4 * 256) {
+        f4 v = f4zero();
+        if (i < nvalid) {
+#pragma unroll 8
+          for (int jt = 0; jt < n_times; ++jt) v += *reinterpret_cast<const f4*>(blk + (size_t)jt * NRL + i);
         }
         *reinterpret_cast<f4*>(tsum + i) = v;
-        if (i2 < BLK) *reinterpret_cast<f4*>(tsum + i2) = v2;
       }
     } else {
       #pragma unroll 1
@@ -2972,50 +2965,38 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
         tsum[i] = v;
       }
     }
-  };
-  // (2) G0[tile]^T x W0SP on MFMA (L2-latency bound): operands in batches of QB k-steps, loaded
-  // unconditionally (column tiles past NST clamp to the last one; their results are never stored)
-  // so a batch's loads are all in flight before its MFMAs -- a guarded load per MFMA serialises on
-  // its latency
-  const float* gb = g0buf + (size_t)tile * M::K0 * TT;
-  const float* wp = pack + M::W0SP_OFF;
-  constexpr int KQ = M::K0 / 4, QB = 8;
-  f4 acc[SPW];
-  auto static_gemm = [&]() {
-    int col[SPW];
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) col[j] = min(w + 4 * j, NST - 1) * 16 + t;
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) acc[j] = f4zero();
-#pragma unroll
-    for (int q0 = 0; q0 < KQ; q0 += QB) {
-      float a[QB], b[QB][SPW];
-#pragma unroll
-      for (int qq = 0; qq < QB; ++qq) {
-        if (q0 + qq < KQ) {
-          const int k = 4 * (q0 + qq) + g;
-          a[qq] = gb[k * TT + t];                      // A[traj t][o = k]
-#pragma unroll
-          for (int j = 0; j < SPW; ++j) b[qq][j] = wp[k * M::S16 + col[j]];
-        }
-      }
-#pragma unroll
-      for (int qq = 0; qq < QB; ++qq)
-        if (q0 + qq < KQ)
-#pragma unroll
-          for (int j = 0; j < SPW; ++j) acc[j] = mfma4(a[qq], b[qq][j], acc[j]);
-    }
-  };
-  // the two parts in opposite orders on alternate tiles: the co-resident workgroups of a CU then
-  // overlap one's HBM stream with another's latency-bound GEMM instead of all streaming, then all waiting
-  if (tile & 1) {
-    static_gemm();
-    time_sums();
-  } else {
-    time_sums();
-    static_gemm();
   }
   __syncthreads();
+  const float* gb = g0buf + (size_t)tile * M::K0 * TT;
+  const float* wp = pack + M::W0SP_OFF;
+  // operands in batches of QB k-steps, loaded unconditionally (column tiles past NST clamp
+  // to the last one; their results are never stored) so a batch's loads are all in flight
+  // before its MFMAs -- a guarded load per MFMA serialises on its latency
+  constexpr int KQ = M::K0 / 4, QB = 8;
+  int col[SPW];
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) col[j] = min(w + 4 * j, NST - 1) * 16 + t;
+  f4 acc[SPW];
+#pragma unroll
+  for (int j = 0; j < SPW; ++j) acc[j] = f4zero();
+#pragma unroll
+  for (int q0 = 0; q0 < KQ; q0 += QB) {
+    float a[QB], b[QB][SPW];
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq) {
+      if (q0 + qq < KQ) {
+        const int k = 4 * (q0 + qq) + g;
+        a[qq] = gb[k * TT + t];                        // A[traj t][o = k]
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) b[qq][j] = wp[k * M::S16 + col[j]];
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < QB; ++qq)
+      if (q0 + qq < KQ)
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) acc[j] = mfma4(a[qq], b[qq][j], acc[j]);
+  }
 #pragma unroll
   for (int j = 0; j < SPW; ++j) {
     const int s = (w + 4 * j) * 16 + t;

@@ -4,8 +4,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd)
-mkdir -p gpurun_out/final4
-O=$R/gpurun_out/final4
+mkdir -p gpurun_out/final5
+O=$R/gpurun_out/final5
 timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > $O/bench_full.json 2> $O/bench_full.err || { tail -20 $O/bench_full.err; exit 21; }
 python3 tools/bench_summary.py $O/bench_full.json
 B="python3 $R/bench.py --no-extra --no-cpu-baseline"

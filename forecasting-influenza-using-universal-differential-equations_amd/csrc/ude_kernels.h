@@ -96,50 +96,9 @@ __device__ __forceinline__ float reg_term(float v) {
 #ifndef UDE_ABL
 #define UDE_ABL 0
 #endif
-// Two interleaved accumulation chains for a wave's single-tile forward / input-gradient phases
-// (-DUDE_DUAL=1).  Off: measured no gain (tools/ab_flags.py, profiles/r04/ab_dual_*.log: M1 Fp [32,32]
-// 3.203 vs 3.196 ms/step, M1 FaFp 7.642 vs 7.623, state49 2.897 vs 2.884 with / without), and it
-// changes the fp32 summation order of those phases
-#ifndef UDE_DUAL
-#define UDE_DUAL 0
-#endif
-// Training forward (large records, 4 waves), -DUDE_FWD_EARLY_ST=1: each layer's activation rows go to
-// HBM during the next layer's phase, issued behind that phase's weight loads.  Off: measured slower
-// (profiles/r04/ab_early_*.log: state49 fwd 1.075 vs 1.041 ms, Bayes state49 1.835 vs 1.742 ms) --
-// the stores then compete with the phases' weight and operand traffic instead of the flux pass
-// training forward (large records): activation-row quads per LDS-read / store batch of the tail copy.
-// All of them at once (state49 fwd 0.936 -> 0.892 ms against batches of 3, profiles/r04/ab_uc_*.log;
-// the tail runs after the layer phases, whose registers are free by then)
-#ifndef UDE_TAIL_UC
-#define UDE_TAIL_UC 16
-#endif
-// split backward kernels, -DUDE_PRIO=1: the critical-path waves run at a raised issue priority
-// (s_setprio 2).  Off: no gain (profiles/r04/ab_prio_*.log: state49 bwd 1.833 vs 1.806 ms, M1 and
-// M1 Fp [32,32] within 0.3%)
-#ifndef UDE_PRIO
-#define UDE_PRIO 0
-#endif
-// large records (R > ~20): the training forward writes each stage's checkpointed input from the
-// record's Y slot as 16-B stores along the trajectories, behind phase 0's weight loads (state49 fwd
-// 0.945 -> 0.925 ms; at R = 1 it cost M1 2%: small records keep three 4-B stores per (trajectory,
-// region) in the flux pass; -DUDE_CKPT_ROWS=0 everywhere, profiles/r04/ab_ck_*.log)
-#ifndef UDE_CKPT_ROWS
-#define UDE_CKPT_ROWS 1
-#endif
-// -DUDE_LAT_ROWS=1: the latent's grid-hit outputs (schedule mode 1) written row-mapped from the
-// record's Y slot during the next step's first layer phase instead of pair-mapped by the flux pass.
-// Off: no gain at state49 (0.925 vs 0.928 ms), 0.2% slower at M1 (profiles/r04/ab_ck_*.log)
-#ifndef UDE_LAT_ROWS
-#define UDE_LAT_ROWS 0
-#endif
-// the forward's row-mapped tile start (fwd_tile_static / fwd_tile_latent); -DUDE_ROWS16=0: the per-pair
-// copy loops (A/B)
-#ifndef UDE_ROWS16
-#define UDE_ROWS16 1
-#endif
-#ifndef UDE_FWD_EARLY_ST
-#define UDE_FWD_EARLY_ST 0
-#endif
+// Measured-off A/B variants of rounds 3-4 (two interleaved accumulation chains, early activation-row
+// stores, row-mapped latent outputs, raised critical-path priority) were
+// removed from the tree: profiles/r04/ab_*.log hold their measurements.
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
@@ -398,13 +357,9 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     hook(dd);
     __builtin_amdgcn_sched_barrier(0);
     f4 acc[M::FT(d) > 0 ? M::FT(d) : 1];
-    // one output tile in this phase: its K chain as two interleaved accumulators (see mlp_backward)
-    constexpr bool DUALF = UDE_DUAL && M::own_phase(W, d) == 1 && M::kin(M::fnet(d, M::first_owned(W, d)), d) >= 32;
-    f4 acc2[DUALF ? M::FT(d) : 1];
     sfor<M::FT(d)>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
       if constexpr (M::fowner(d, k) == W) {
-        if constexpr (DUALF) acc2[k] = f4zero();
         if constexpr (d == 0 && M::HOIST) acc[k] = c1[M::nz_before(W, k)];
         else if constexpr (RW) acc[k] = wr.wb[M::nb_base(W, d) + M::nb_before(W, d, k)];
         else acc[k] = bias[k];
@@ -456,7 +411,6 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
                   if constexpr (CHUNK_A) wq = fa[cb][CHUNK_A ? k : 0][CHUNK_A ? q - q0 : 0];
                   else wq = FR(M::fq_before(W, d, k) + q);
                   if constexpr (UDE_ABL == 13) acc[k][e] += x[e];
-                  else if (DUALF && (e & 1)) acc2[DUALF ? k : 0] = mfma4(wq[e], x[e], acc2[DUALF ? k : 0]);
                   else acc[k] = mfma4(wq[e], x[e], acc[k]);
                 }
               });
@@ -469,7 +423,6 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
       if constexpr (M::fowner(d, k) == W) {
         constexpr int net = M::fnet(d, k), rt = M::frt(d, k);
         f4 a = acc[k];
-        if constexpr (DUALF) a = a + acc2[k];
         if constexpr (M::act(net, d)) {
           a[0] = elu1(a[0]); a[1] = elu1(a[1]);
           a[2] = elu1(a[2]); a[3] = elu1(a[3]);
@@ -590,37 +543,6 @@ __device__ __forceinline__ size_t ckpt_index(int tile, int n_steps, int step, in
   return ((((size_t)tile * n_steps + step) * 4 + stage) * F + f) * TT + t;
 }
 
-// The grid-hit outputs (mode 1) of RK step `step` -- y_{step+1}, the record's Y slot from the flux
-// barrier of the step's last stage until the next one -- row-mapped: consecutive lanes write the S, I, R
-// of consecutive (n, r) rows of the tile's contiguous (16, R, L) block (the flux pass's pair mapping
-// put consecutive lanes R * L floats apart).
-template <class M, int SR>
-__device__ __forceinline__ void store_latent_rows(const KArgs& A, const Sched& sc, const float* lds, int n0,
-                                                  int step, int tid) {
-  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS;
-  asm volatile("" : "+v"(tid));
-  const int nvalid = min(TT, A.n_traj - n0) * M::R;
-  const size_t NRL = (size_t)A.n_traj * M::R * M::L;
-  const int o_end = sc.out_start[step + 1];
-  #pragma unroll 1
-  for (int o = sc.out_start[step]; o < o_end; ++o) {
-    if (sc.out_mode[o] != 1) continue;
-    float* base = A.latent + (size_t)sc.out_j[o] * NRL + (size_t)n0 * M::R * M::L;
-#pragma unroll
-    for (int u = 0; u < PR; ++u) {
-      const int i = tid + u * NTHREADS;
-      if (i < nvalid) {
-        const int t = i / M::R, r = i - t * M::R;
-        const float* y = lds + t * SR + M::Y_OFF + 3 * r;
-        float* d = base + (size_t)i * M::L;
-        d[0] = y[0];
-        d[1] = y[1];
-        d[2] = y[2];
-      }
-    }
-  }
-}
-
 // The stage input in the record's Y slot ([16][F] at Y_OFF) -> its checkpoint block ([F][16]): lane
 // (f, q) gathers trajectories 4q .. 4q + 3 of feature f (conflict-free LDS reads: consecutive lanes,
 // consecutive banks) and writes them as one 16-B store; 64 lanes cover 1 KB of the block.
@@ -670,34 +592,6 @@ __host__ __device__ __forceinline__ int act_src_q(int i) {
   constexpr int QR = M::ACT_A4 / 4;
   if constexpr (M::XST_W == M::ACT_A4) return i;
   else return (i / QR) * (M::XST_W / 4) + M::ACT_IN / 4 + (i - (i / QR) * QR);
-}
-
-// Record columns [ACT0 + 4 LQ, ACT0 + 4 (LQ + NQL)) of the tile's 16 trajectories -> their stored
-// activation rows (one layer's outputs; 16-B LDS reads, 16-B global stores).
-template <class M, int SR, int LQ, int NQL>
-__device__ __forceinline__ void store_act_cols(float* blk, const float* lds, int tid) {
-  constexpr int PER = (TT * NQL + NTHREADS - 1) / NTHREADS;
-  f4* dst = reinterpret_cast<f4*>(blk);
-  // thread-derived addresses formed here, not hoisted out of the stage loop into registers the
-  // layer phases need (the forward is at the 256-VGPR limit)
-  asm volatile("" : "+v"(tid));
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int i = tid + u * NTHREADS;
-    if (i < TT * NQL) {
-      const int t = i / NQL, q = LQ + (i - t * NQL);
-      dst[t * (M::XST_W / 4) + M::ACT_IN / 4 + q] = *reinterpret_cast<const f4*>(lds + t * SR + M::ACT0 + 4 * q);
-    }
-  }
-}
-// layer j's rows of every net that has a layer j
-template <class M, int SR, int J>
-__device__ __forceinline__ void store_act_layer(float* blk, const float* lds, int tid) {
-  sfor<2>([&](auto nn) {
-    constexpr int net = decltype(nn)::value;
-    if constexpr (J < M::nl(net))
-      store_act_cols<M, SR, (M::act_off(net, J) - M::ACT0) / 4, M::kout(net, J) / 4>(blk, lds, tid);
-  });
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -780,9 +674,11 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 
     // the row-mapped tile start (fwd_tile_static / fwd_tile_latent; L = 8: 16-B latent rows, checked by
     // the host entry)
-    constexpr bool rows16 = UDE_ROWS16 && M::L == 8;
-    constexpr bool LAT_ROWS = UDE_LAT_ROWS && !DEC;
-    constexpr bool CKR = UDE_CKPT_ROWS && SL > 1;           // large records: checkpoint rows
+    constexpr bool rows16 = M::L == 8;
+    // large records: each stage's checkpointed input written as 16-B rows from the Y slot behind phase 0's
+    // weight loads (state49 fwd 0.945 -> 0.925 ms); small records keep three 4-B stores per (trajectory,
+    // region) in the flux pass (rows cost M1 2%; profiles/r04/ab_ck_*.log)
+    constexpr bool CKR = SL > 1;
     if constexpr (rows16) fwd_tile_static<M, SR, M::XSF_OFF>(A, lds, n0);
     // y0 -> registers, LDS Y slot, latent[0], ckpt(step 0, stage 0)
     sfor<SL>([&](auto ss) {
@@ -854,44 +750,27 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         if constexpr (PFB) {
           if (step == 0 && j == 0) wr.load(rse, lane, false);        // the tile's first evaluation
         }
-        constexpr bool EARLY_ST = TRAIN && M::ACT_STORED && !SPLIT && !M::STORE_ACT && UDE_FWD_EARLY_ST && UDE_ABL != 11;
-        if constexpr (EARLY_ST) {
-          // layer d - 1's rows during phase d, behind its weight loads: a later wait on those loads
-          // (in-order vmcnt) then does not also wait for these stores to complete
-          float* blk = act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j);
-          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
-            constexpr int d = decltype(dd)::value;
-            if constexpr (d >= 1) store_act_layer<M, SR, d - 1>(blk, lds, tid);
-            if constexpr (d == 0 && CKR)
+        // this stage's input (the record's Y slot, layer 0's input) -> its checkpoint, issued behind
+        // phase 0's weight loads (their waits then do not wait for these stores) and read before
+        // the phase's barrier (the flux pass overwrites the slot after the last phase)
+        mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
+          if constexpr (decltype(dd)::value == 0) {
+            if constexpr (TRAIN && CKR)
               store_ckpt_rows<M, SR>(A.ckpt + ckpt_index(tile, A.n_steps, step, j, M::F, 0, 0), lds, tid);
-          });
-          store_act_layer<M, SR, M::D - 1>(blk, lds, tid);
-        } else {
-          // this stage's input (the record's Y slot, layer 0's input) -> its checkpoint, issued behind
-          // phase 0's weight loads (their waits then do not wait for these stores) and read before
-          // the phase's barrier (the flux pass overwrites the slot after the last phase)
-          mlp_forward<M, W, SR>(rse, lds, c1, lane, wr, pf, [&](auto dd) {
-            if constexpr (decltype(dd)::value == 0) {
-              if constexpr (TRAIN && CKR)
-                store_ckpt_rows<M, SR>(A.ckpt + ckpt_index(tile, A.n_steps, step, j, M::F, 0, 0), lds, tid);
-              // the previous step's grid-hit outputs (y_step, this stage's input)
-              if constexpr (LAT_ROWS) {
-                if (j == 0 && step > 0) store_latent_rows<M, SR>(A, sc, lds, n0, step - 1, tid);
-              }
-            }
-          });
-        }
+          }
+        });
         if constexpr (PFB) {
           const int en = 4 * step + j + 1;
           if (en < 4 * A.n_steps) wr.load(make_rsrc(A.pack + (size_t)en * M::PACK_TOTAL, M::PACK_TOTAL * 4), lane, false);
         }
-        if constexpr (TRAIN && M::ACT_STORED && !SPLIT && !EARLY_ST && UDE_ABL != 11) {
+        if constexpr (TRAIN && M::ACT_STORED && !SPLIT && UDE_ABL != 11) {
           // this stage's activation rows -> HBM for the backward (read before the flux barrier;
           // the stores drain behind the rest of the stage)
           f4* dst = reinterpret_cast<f4*>(act_block<M>(A.ckpt, A.n_tiles, A.n_steps, tile, step, j));
           constexpr int QR = M::ACT_A4 / 4, NQ = act_q_per_thread<M>();
-          // UC quads per batch (UDE_TAIL_UC; the forward runs two workgroups per CU: 256 registers)
-          constexpr int UC = NQ <= 5 ? NQ : cmin(NQ, UDE_TAIL_UC);
+          // all of a thread's LDS reads, then all its 16-B stores (state49 fwd 0.936 -> 0.892 ms against
+          // batches of 3 quads, profiles/r04/ab_uc_*.log: the phases' registers are free by then)
+          constexpr int UC = NQ <= 5 ? NQ : cmin(NQ, 16);
           #pragma unroll 1
           for (int u0 = 0; u0 < NQ; u0 += UC) {
 #pragma unroll
@@ -983,7 +862,6 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
                 #pragma unroll 1
                 for (int o = sc.out_start[step]; o < o_end; ++o) {
                   const int jo = sc.out_j[o], mode = sc.out_mode[o];
-                  if (LAT_ROWS && mode == 1) continue;       // store_latent_rows, next step
                   const float slope = sc.out_slope[o];
                   float* dst = A.latent + (size_t)jo * NRL + ((size_t)n * M::R + r) * M::L;
 #pragma unroll
@@ -1017,12 +895,6 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
       if constexpr (DEC) {
         if (sc.out_start[step] < sc.out_start[step + 1]) dec_emit(sc.out_j[sc.out_start[step]]);
       }
-    }
-    if constexpr (LAT_ROWS) {
-      // the last step's grid-hit outputs; the next tile's stage input overwrites the Y slot after
-      // this barrier
-      if (A.n_steps > 0) store_latent_rows<M, SR>(A, sc, lds, n0, A.n_steps - 1, tid);
-      lds_sync();
     }
   }
 
@@ -1082,7 +954,6 @@ __device__ void fwd_sbody(const KArgs& A, float* lds) {
         lds_sync();                            // flux pass (the next stage rewrites the rows)
       }
     }
-    if constexpr (UDE_LAT_ROWS && !DEC) lds_sync();   // the last step's latent rows
   }
   lds_sync();                                  // side-statistic reduction
   lds_sync();
@@ -1372,16 +1243,10 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       return;
     }
     f4 avv[M::XT(d) > 0 ? M::XT(d) : 1];
-    // a wave with a single input-gradient tile in this phase runs its K chain as two interleaved
-    // accumulation chains (even / odd k quads): the chain is latency-bound there (40 cycles per
-    // dependent v_mfma_f32_16x16x4_f32 against a 32-cycle issue), with two it is issue-bound
-    constexpr bool DUALX = UDE_DUAL && M::own_x(W, d) == 1;
-    f4 xo[DUALX ? M::XT(d) : 1];
     sfor<M::XT(d)>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
         xa[m] = f4zero();
-        if constexpr (DUALX) xo[m] = f4zero();
         if constexpr (d > 0) {
           // the ELU-derivative operand of the epilogue, read ahead of the MFMAs
           constexpr int net = M::xnet(d, m), rt = M::xrt(d, m);
@@ -1410,7 +1275,6 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
               constexpr int m = decltype(mm)::value;
               if constexpr (M::xowner(d, m) == W && (d == 0 || M::xnet(d, m) == net)) {
                 if constexpr (UDE_ABL == 3) xa[m][e] += x[e];
-                else if (DUALX && (e & 1)) xo[DUALX ? m : 0] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xo[DUALX ? m : 0]);
                 else xa[m] = mfma4(FX(M::xq_before(W, d, m) + qoff + q)[e], x[e], xa[m]);
               }
             });
@@ -1422,7 +1286,6 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
       constexpr int m = decltype(mm)::value;
       if constexpr (M::xowner(d, m) == W) {
         f4 acc = xa[m];
-        if constexpr (DUALX) acc = acc + xo[m];
         if constexpr (d == 0) {
           ep0(m * 16 + g * 4, acc);
         } else {
@@ -2645,9 +2508,6 @@ __global__ __launch_bounds__(M::BWD_THREADS) void ude_bwd_kernel(KArgs a) {
       return;
     }
   }
-  // UDE_PRIO: the critical-path waves win the issue arbitration against their partner waves on the
-  // same SIMD (tried because either stream alone takes 1.45 ms, both 1.94: profiles/r04/abl3_state49_bwd.log)
-  if constexpr ((M::SPLIT_BWD || M::SPLIT_BWD_L) && UDE_PRIO) __builtin_amdgcn_s_setprio(2);
   if (w == 0) bwd_body<M, 0>(a, lds);
   else if (w == 1) bwd_body<M, 1>(a, lds);
   else if (w == 2) bwd_body<M, 2>(a, lds);

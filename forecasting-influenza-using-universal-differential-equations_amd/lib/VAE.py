@@ -18,10 +18,12 @@ On a HIP device a training call runs the solve with the decoder epilogue
 (ude_amd/decoder_head.py): the forward kernel emits the decoder output
 y_hat = Decoder(latent[..., :3]) and latent_init_loss(latent[..., :3]) at every output time and
 writes no (T, N, R, L) latent -- ``self.latent`` is rebuilt from the training store only when it
-is read -- and calc_loss takes nll_loss of that prediction from the gfx950 nll kernels.  When
-the epilogue does not apply (output times between grid points, Bayesian RHS, a non-reference
-decoder) the latent is written and the fused loss head (ude_amd/loss_head.py: decoder +
-nll_loss + latent_init_loss in one kernel pass each) serves the same terms.
+is read -- and calc_loss takes nll_loss of that prediction from the gfx950 nll kernels.  The
+Bayesian RHS (models_bayes.py, run_ode.py's ``*b`` models) takes the same epilogue
+(``fused.FusedBayesRK4Dec``: each evaluation's weight sample through the decoder forward).  When
+the epilogue does not apply (output times between grid points, a non-reference decoder) the latent
+is written and the fused loss head (ude_amd/loss_head.py: decoder + nll_loss + latent_init_loss in
+one kernel pass each) serves the same terms.
 """
 from itertools import chain
 

@@ -307,10 +307,17 @@ def _run(cmd: List[str]) -> None:
         raise UdeError("build command failed:\n" + " ".join(cmd) + "\n" + r.stdout[-8000:])
 
 
-def source_hash() -> str:
+_SRC_HASH: Optional[str] = None
+
+
+def source_hash(fresh: bool = False) -> str:
     """sha1 (16 hex digits) of every source the library is compiled from (csrc/*.h, csrc/*.hip,
     include/ude_rk4.h) and of the compile flags.  Embedded in ``ude_build_info`` so a prebuilt
-    library that no longer matches the tree is refused at load (``prebuilt``)."""
+    library that no longer matches the tree is refused at load (``prebuilt``).  Computed once per
+    process (the tree the process started from); ``fresh`` re-reads the sources (the builder)."""
+    global _SRC_HASH
+    if _SRC_HASH is not None and not fresh:
+        return _SRC_HASH
     srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip")))
     srcs.append(os.path.join(INCLUDE, "ude_rk4.h"))
     h = hashlib.sha1()
@@ -319,10 +326,16 @@ def source_hash() -> str:
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(" ".join(HIP_FLAGS).encode())
-    return h.hexdigest()[:16]
+    _SRC_HASH = h.hexdigest()[:16]
+    return _SRC_HASH
 
 
 _INFO_HASH = re.compile(r"\bsrc=([0-9a-f]+)")
+_INFO_EXTRA = re.compile(r"\bextra_flags=\[(.*)\]")
+
+
+def _c_string(s: str) -> str:
+    return s.replace("\\", "\\\\").replace('"', '\\"')
 
 
 def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: Optional[int] = None,
@@ -338,8 +351,8 @@ def build_library(cfgs: Sequence[_cfgs.Config], out_path: str, tag: str, jobs: O
     reg.append(f"constexpr int kNumEntries = {len(cfgs)};")
     reg.append("}  // namespace ude")
     reg.append(f'#define UDE_REGISTRY_TAG "{tag}:{len(cfgs)}"')
-    reg.append(f'#define UDE_SRC_HASH "{source_hash()}"')
-    reg.append(f'#define UDE_EXTRA_FLAGS "{" ".join(extra_flags)}"')
+    reg.append(f'#define UDE_SRC_HASH "{source_hash(fresh=True)}"')
+    reg.append(f'#define UDE_EXTRA_FLAGS "{_c_string(" ".join(extra_flags))}"')
     with open(os.path.join(gen, "ude_registry.inc"), "w") as f:
         f.write("\n".join(reg) + "\n")
     inc = ["-I", INCLUDE, "-I", CSRC, "-I", gen, *extra_flags]
@@ -387,16 +400,27 @@ def built_hash(lib: NativeLib) -> Optional[str]:
     return m.group(1) if m else None
 
 
+_verified: Dict[str, bool] = {}
+
+
 def prebuilt() -> NativeLib:
     """The in-tree prebuilt library; refused if it was built from other sources than the tree's
-    (a stale binary would silently run old kernels)."""
+    (a stale binary would silently run old kernels) or with extra compile flags (an A/B or
+    diagnostic build -- -DUDE_ABL, -DUDE_PROFILE -- placed at the product path).  Checked once per
+    process: the library a process has loaded does not change when the sources are edited."""
     if not os.path.exists(PREBUILT_LIB):
         raise UdeError(f"{PREBUILT_LIB} is missing: run __graft_entry__.build() (hipcc, gfx950)")
     lib = _load(PREBUILT_LIB)
-    got, want = built_hash(lib), source_hash()
-    if got != want:
-        raise UdeStaleLibrary(f"{PREBUILT_LIB} is stale (built from sources {got}, tree is {want}): "
-                       "rebuild it with __graft_entry__.build()")
+    if not _verified.get(PREBUILT_LIB):
+        got, want = built_hash(lib), source_hash()
+        if got != want:
+            raise UdeStaleLibrary(f"{PREBUILT_LIB} is stale (built from sources {got}, tree is {want}): "
+                                  "rebuild it with __graft_entry__.build()")
+        m = _INFO_EXTRA.search(lib.build_info())
+        if m is None or m.group(1).strip():
+            raise UdeStaleLibrary(f"{PREBUILT_LIB} was built with extra flags [{m.group(1) if m else '?'}] "
+                                  "(a development build): rebuild it with __graft_entry__.build()")
+        _verified[PREBUILT_LIB] = True
     return lib
 
 

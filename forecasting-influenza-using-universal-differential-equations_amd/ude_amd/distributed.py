@@ -86,7 +86,12 @@ def broadcast_parameters(params: Iterable[torch.nn.Parameter], src: int = 0, gro
 
 def broadcast_rng_state(device, src: int = 0, group=None) -> None:
     """Rank src's RNG state (the host generator and, for a HIP device, that device's) on every
-    rank, so replicated random draws (the VAE's full-batch eps) agree without per-step traffic."""
+    rank, so replicated random draws (the VAE's full-batch eps) agree without per-step traffic.
+
+    This synchronises the process-wide generators: from the call on, every torch draw (the VAE's
+    eps, but also dropout or any other sampling of the caller) is identical on every rank.  The
+    data-parallel VAE step relies on exactly that (each rank slices the same full-batch eps);
+    code that needs per-rank randomness after it must use its own ``torch.Generator``."""
     if not _active(group):
         return
     dev = torch.device(device)
@@ -148,10 +153,9 @@ def _sync_from_sums(module, group) -> bool:
     for e in sums[1:]:
         local = local + stat_sums(e[1], e[2], e[0])
     n_tot, gm, gs, gn = combine_sums(n, local, group)
-    module.params = []
-    module._fused_sums = []
+    dt = module._fused_rates[0][1].dtype if has_p else None
+    module.params = []                      # drops the local statistics (and their sums)
     if has_p:
-        dt = module._fused_rates[0][1].dtype
         module._fused_rates = [(n_tot.detach(), gm.to(dt), gs.to(dt))]
     if has_a:
         module.tracker = [gn.to(module.tracker[0].dtype)]

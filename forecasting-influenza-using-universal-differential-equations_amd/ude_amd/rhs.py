@@ -117,12 +117,25 @@ class _UDEModule(nn.Module):
         # (n_eval, stats, fp64 sums) of every fused solve that reported its sums (``_record_fused``)
         self._fused_sums: List[Tuple[float, torch.Tensor, torch.Tensor]] = []
 
-    def clear_tracking(self):
-        """Resets the trackers (lib/models.py:148-150)."""
-        self.params = []
-        self.tracker = []
+    # ``params`` is the list of recorded rates (lib/models.py:137).  A fused solve records its rates
+    # as sufficient statistics (``_fused_rates``) next to that list, so assigning a new list -- the
+    # reference's reset idiom ``ode.params = []`` (tuning/tune_Fp.py:88), which drops every rate the
+    # module has recorded -- drops those statistics too; ``posterior()`` then pools only the solves
+    # that ran after the assignment, as the reference's list does.
+    @property
+    def params(self):
+        return self._params
+
+    @params.setter
+    def params(self, value):
+        self._params = value
         self._fused_rates = []
         self._fused_sums = []
+
+    def clear_tracking(self):
+        """Resets the trackers (lib/models.py:148-150)."""
+        self.params = []              # also drops the fused solves' rate statistics
+        self.tracker = []
 
     # -- fused-solver side statistics ------------------------------------------
     def _record_fused(self, stats: torch.Tensor, n_eval: int, evals=None, sums=None) -> None:
@@ -139,7 +152,7 @@ class _UDEModule(nn.Module):
             self._fused_rates.append((float(n_eval), s_mean, s_std))
             if evals is not None:
                 if not isinstance(self.params, _FusedList):
-                    self.params = _FusedList(self.params)
+                    self._params = _FusedList(self.params)     # the same rates: no reset
                 entries = evals[0].unbind(0)
                 self.params.extend(entries)
                 self.params.fused_ids.update(id(e) for e in entries)
@@ -182,9 +195,7 @@ class _UDEModule(nn.Module):
             p = torch.stack(eager).reshape(-1, 2)
             groups.append((float(p.shape[0]), p.mean(0), p.std(0)))
         groups.extend(self._fused_rates)
-        self.params = []
-        self._fused_rates = []
-        self._fused_sums = []
+        self.params = []              # clears the fused solves' statistics with the list
         if not groups:
             torch.stack([])  # same error as the reference on an empty tracker
         if len(groups) == 1:

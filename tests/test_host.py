@@ -160,10 +160,37 @@ def test_prebuilt_library_matches_the_tree(native):
 
 def test_stale_prebuilt_library_is_refused(native, monkeypatch):
     lib = native.prebuilt()
-    monkeypatch.setattr(native, "source_hash", lambda: "0" * 16)
+    monkeypatch.setattr(native, "source_hash", lambda *a, **k: "0" * 16)
+    monkeypatch.setattr(native, "_verified", {})
     with pytest.raises(native.UdeStaleLibrary):
         native.prebuilt()
     native._SUPPORTED.clear()
     with pytest.raises(native.UdeStaleLibrary):      # not silently reported as "unsupported"
         native.config_supported(native._cfgs.PREBUILT[0])
     native._SUPPORTED.clear()
+
+
+def test_prebuilt_check_runs_once_per_process(native, monkeypatch):
+    """library_for() runs every training step; the source hash is read once per process
+    and the loaded library verified once (editing a source mid-run does not fail the next step)."""
+    native.prebuilt()
+    calls = []
+    monkeypatch.setattr(native, "source_hash", lambda *a, **k: calls.append(1) or "0" * 16)
+    for _ in range(3):
+        native.prebuilt()
+    assert calls == []
+    assert native.source_hash.__name__ == "<lambda>"
+
+
+def test_development_build_at_product_path_is_refused(native, monkeypatch):
+    """a library built with extra flags (-DUDE_ABL, -DUDE_PROFILE ...) carries the same
+    source hash; prebuilt() refuses it by its recorded extra flags."""
+    lib = native.prebuilt()
+    info = lib.build_info()
+    assert "extra_flags=[]" in info
+    monkeypatch.setattr(native, "_verified", {})
+    monkeypatch.setattr(native.NativeLib, "build_info", lambda self: info.replace("extra_flags=[]",
+                                                                                   "extra_flags=[-DUDE_ABL=14]"))
+    with pytest.raises(native.UdeStaleLibrary):
+        native.prebuilt()
+    assert native._c_string('a "b" \\c') == 'a \\"b\\" \\\\c'

@@ -83,6 +83,53 @@ def test_materialized_lists_match_eager_solve(pkg, kind):
         assert normwise_rel(g_f[k], g_s[k]) < 1e-5, k
 
 
+def test_params_reset_drops_fused_statistics_host(pkg):
+    """the reference's reset idiom ``ode.params = []`` (tuning/tune_Fp.py:88) drops
+    every rate recorded before it -- also the sufficient statistics a fused solve records instead of
+    list entries (host check of the bookkeeping; the GPU test below runs the solves)."""
+    mod = pkg.Fp(1, latent_dim=8, net_sizes=[32, 32])
+    s1 = torch.tensor([0.5, 0.2, 0.1, 0.05, 0.0])
+    s2 = torch.tensor([0.7, 0.3, 0.2, 0.1, 0.0])
+    mod._record_fused(s1, 100, sums=torch.zeros(5, dtype=torch.float64))
+    mod.params = []
+    assert mod._fused_rates == [] and mod._fused_sums == []
+    mod._record_fused(s2, 100)
+    post = mod.posterior()
+    assert torch.equal(post.loc, s2[:2]) and torch.equal(post.scale, s2[2:4])
+    # a list that is only appended to keeps pooling (posterior() over both solves)
+    mod._record_fused(s1, 100)
+    mod.params.append(torch.full((3, 1, 2), 0.5))
+    post = mod.posterior()
+    assert post.loc.shape == (2,) and mod.params == [] and mod._fused_rates == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["FaFp", "Fp"])
+def test_params_reset_between_fused_solves(pkg, kind):
+    """tuning/tune_Fp.py:88-93 on the fused path: a solve, ``ode.params = []``, a second solve ->
+    posterior() equals the posterior of the second solve alone (the reference's list semantics),
+    gradients included."""
+    mod, y0, t = _case(pkg, kind, "cuda")
+    h = t[1] - t[0]
+    y1 = (y0.detach() * 0.97).requires_grad_(True)
+
+    def second_only():
+        mod.clear_tracking()
+        pkg.odeint(mod, y1, t, method="rk4", options=dict(step_size=h))
+        return mod.posterior()
+
+    ref = second_only()
+    mod.clear_tracking()
+    pkg.odeint(mod, y0, t, method="rk4", options=dict(step_size=h))
+    mod.params = []
+    pkg.odeint(mod, y1, t, method="rk4", options=dict(step_size=h))
+    got = mod.posterior()
+    assert torch.equal(got.loc, ref.loc) and torch.equal(got.scale, ref.scale)
+    (got.loc.sum() + got.scale.sum()).backward()
+    assert y0.grad is None or float(y0.grad.abs().max()) == 0.0     # the dropped solve gets no gradient
+    assert y1.grad is not None and float(y1.grad.abs().max()) > 0.0
+
+
 @pytest.mark.gpu
 def test_materialized_then_eager_evaluation_pooled(pkg):
     """A fused solve with materialised lists followed by a direct evaluation of the module

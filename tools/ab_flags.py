@@ -3,7 +3,7 @@ flags.  `--build` on the host builds every variant; without it, on the GPU box, 
 step with each (interleaved rounds, so drift hits every variant alike) and prints the kernel
 times and each variant's largest normwise gradient difference from the first.
 
-  AB_WORKLOAD=us_fp32 AB_VARIANTS="dual0:;dual1:-DUDE_DUAL=1" python tools/ab_flags.py [--build]
+  AB_WORKLOAD=us_fp32 AB_VARIANTS="a:;b:-DUDE_ABL=14" python tools/ab_flags.py [--build]
 """
 import importlib
 import os
@@ -20,7 +20,7 @@ import bench  # noqa: E402
 
 WL = os.environ.get("AB_WORKLOAD", "us_fp32")
 VARIANTS = {}
-for item in os.environ.get("AB_VARIANTS", "dual0:;dual1:-DUDE_DUAL=1").split(";"):
+for item in os.environ.get("AB_VARIANTS", "a:;b:-DUDE_ABL=14").split(";"):
     name, _, flags = item.partition(":")
     VARIANTS[name] = flags.split()
 

@@ -1,14 +1,13 @@
-# Round-3 measurement set (GPU box): full -m gpu suite, the default bench line (all extra lines),
-# rocprof kernel stats (state49, north-star M1, Bayes state49), FETCH / WRITE PMC passes of the
+# Measurement set (GPU box): the default bench line (all extra lines + CPU baselines), rocprof
+# kernel stats (state49, north-star M1, M1 Fp [32,32], Bayes state49), FETCH / WRITE PMC passes of the
 # default line, stage breakdowns.  UDE_COMMIT tags the PMC summaries with the measured commit.
 set -o pipefail
 export TMPDIR=/tmp
 R=$(pwd)
-mkdir -p gpurun_out/final
-O=$R/gpurun_out/final
-timeout -k 10 700 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 20; }
-tail -2 $O/pytest_gpu.log
-timeout -k 10 500 python -u bench.py --steps 10 --warmup 3 > $O/bench_full.json 2> $O/bench_full.err || { tail -20 $O/bench_full.err; exit 21; }
+OUT=${OUT:-gpurun_out/measure}
+mkdir -p $OUT
+O=$R/$OUT
+timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > $O/bench_full.json 2> $O/bench_full.err || { tail -20 $O/bench_full.err; exit 21; }
 python3 tools/bench_summary.py $O/bench_full.json
 B="python3 $R/bench.py --no-extra --no-cpu-baseline"
 cd /tmp
@@ -18,6 +17,8 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/k
 find /tmp/ks2 -name "*kernel_stats.csv" -exec cp {} $O/m1_kernel_stats.csv \;
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks3 -o ks -- $B --workload us_fp32 --steps 5 --warmup 2 > $O/ks3.log 2>&1 || exit 13
 find /tmp/ks3 -name "*kernel_stats.csv" -exec cp {} $O/m1_fp32_kernel_stats.csv \;
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks4 -o ks -- $B --workload bayes_state49 --steps 5 --warmup 2 > $O/ks4.log 2>&1 || exit 16
+find /tmp/ks4 -name "*kernel_stats.csv" -exec cp {} $O/bayes49_kernel_stats.csv \;
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d /tmp/pf -o pf -- $B --steps 3 --warmup 1 > $O/pf.log 2>&1 || exit 14
 mkdir -p $O/pmc_fetch $O/pmc_write
 find /tmp/pf -name "*counter_collection.csv" -exec cp {} $O/pmc_fetch/ \;

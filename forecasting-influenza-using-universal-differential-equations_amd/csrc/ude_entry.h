@@ -64,6 +64,8 @@ struct Ops {
     if constexpr (M::GST)
       HIPCHK(hipFuncSetAttribute((const void*)&ude_gst_dw_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  Gst<M>::LDS));
+    HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_tail_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               Tail<M>::LDS));
     if constexpr (M::FWD_RES) {
       HIPCHK(hipFuncSetAttribute((const void*)&ude_fwd_kernel<M, true, false, false, true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX));
@@ -97,8 +99,12 @@ struct Ops {
   // grad-slab workspace tail (HOIST): G0 [tile][K0][16] + split-K partials [chunks][K0][S16]
   static int64_t static_ws_floats(int n_tiles) {
     if (!M::HOIST) return 0;
-    return (int64_t)n_tiles * M::K0 * TT + (int64_t)M::STATIC_CHUNKS * M::K0 * M::S16;
+    const int64_t legacy = (int64_t)M::STATIC_CHUNKS * M::K0 * M::S16, tail = Tail<M>::part_floats();
+    return (int64_t)n_tiles * M::K0 * TT + (legacy > tail ? legacy : tail);
   }
+  // control words of the *_ex calls: [0] the forward's arrival counter, [1 + st] the tail's static
+  // column tiles (include/ude_rk4.h)
+  static constexpr int64_t CTL_WORDS = 1 + Tail<M>::NST;
 
   // the resident-weight forward (one workgroup per CU) when every tile has a CU of its own;
   // UDE_FWD_RES=0 turns it off, =2 forces it at any batch (A/B measurement)
@@ -190,6 +196,7 @@ struct Ops {
     o->ckpt_final_bytes = (int64_t)n_tiles * M::F * TT * 4;
     o->dec_ws_bytes = (int64_t)gd * LossDims<M::R>::SLAB * 4;
     o->act_bytes = M::ACT_STORED ? (int64_t)n_tiles * p->n_steps * 4 * TT * M::XST_W * 4 : 0;
+    o->ctl_bytes = ((CTL_WORDS * 4 + 63) / 64) * 64;
     return UDE_OK;
   }
 
@@ -216,15 +223,17 @@ struct Ops {
 
   // Training forward with the decoder epilogue: y_hat (T, N, R) and latent_init_loss instead of the
   // latent; ckpt (ckpt_bytes + ckpt_final_bytes) also receives the final state.
+  // stats: mean / std / fa_norm outputs (sums nullable); ctl: null = the separate finalize launches
   static int forward_dec(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
                          const float* dec_pack, float* yhat, float* ckpt, double* stats_slab, double* reg_slab,
-                         float* stats_out, float* reg_out, hipStream_t s) {
+                         const UdeSideStats* st, unsigned* ctl, float* reg_out, hipStream_t s) {
     if constexpr (RC_VIEW) {
       if (p->recompute)
         return Ops<Recompute<M>>::forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab,
-                                              stats_out, reg_out, s);
+                                              st, ctl, reg_out, s);
     }
-    if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !stats_out || !reg_out)
+    if (!pack || !sched || !y0 || !dec_pack || !yhat || !ckpt || !stats_slab || !reg_slab || !reg_out ||
+        !stats_ok(st))
       return UDE_E_INVALID;
     if (p->n_steps < 1) return UDE_E_INVALID;
     int dev = 0;
@@ -241,6 +250,9 @@ struct Ops {
     a.ckpt_final = ckpt + ckpt_final_off<M>(n_tiles, p->n_steps);
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
+    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
+    set_stats_out(a, st, ctl, n_eval);
+    a.o_reg = reg_out;
     int cus = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     // the resident-weight forward runs one workgroup per CU (min(n_tiles, cus) <= gf slabs)
@@ -252,11 +264,13 @@ struct Ops {
       hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true, M::FWD_RES>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, true, false, true>), dim3(gf), dim3(NTHREADS), M::LDS_F_DEC, s, a);
     HIPCHK(hipGetLastError());
-    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, stats_out);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(ude_sum_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)reg_slab, gf, reg_out);
-    HIPCHK(hipGetLastError());
+    if (!ctl) {
+      hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, a.o_mean,
+                         a.o_std, a.o_norm);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL(ude_sum_finalize_kernel<0>, dim3(1), dim3(64), 0, s, (const double*)reg_slab, gf, reg_out);
+      HIPCHK(hipGetLastError());
+    }
     return UDE_OK;
   }
 
@@ -374,13 +388,27 @@ struct Ops {
     return UDE_OK;
   }
 
+  // every statistic of the model's nets needs a buffer (an absent net's may be null)
+  static bool stats_ok(const UdeSideStats* st) {
+    return st && (!M::HAS_P || (st->mean && st->std)) && (!M::HAS_A || st->fa_norm);
+  }
+  static void set_stats_out(KArgs& a, const UdeSideStats* st, unsigned* ctl, double n_eval) {
+    a.o_mean = st->mean;                  // an absent net's buffers may be null: not written
+    a.o_std = st->std;
+    a.o_norm = st->fa_norm;
+    a.o_sums = st->sums;
+    a.ctl = ctl;
+    a.n_eval = n_eval;
+  }
+
   static int forward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
-                     float* latent, float* ckpt, double* stats_slab, float* stats_out, hipStream_t s) {
+                     float* latent, float* ckpt, double* stats_slab, const UdeSideStats* st, unsigned* ctl,
+                     hipStream_t s) {
     if constexpr (RC_VIEW) {
       if (p->recompute && ckpt) return Ops<Recompute<M>>::forward(p, pack, sched, y0, latent, ckpt, stats_slab,
-                                                                  stats_out, s);
+                                                                  st, ctl, s);
     }
-    if (!pack || !sched || !y0 || !latent || !stats_slab || !stats_out) return UDE_E_INVALID;
+    if (!pack || !sched || !y0 || !latent || !stats_slab || !stats_ok(st)) return UDE_E_INVALID;
     if (M::L == 8 && (reinterpret_cast<uintptr_t>(latent) & 15))
       return UDE_E_INVALID;                          // the row-mapped tile start writes 16-B latent rows
     int dev = 0;
@@ -395,6 +423,8 @@ struct Ops {
     a.latent = latent; a.ckpt = ckpt; a.stats_slab = stats_slab;
     a.n_traj = p->n_traj; a.n_steps = p->n_steps; a.n_out = p->n_out; a.n_tiles = n_tiles;
     a.fa_w = p->fa_w;
+    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
+    set_stats_out(a, st, ctl, n_eval);
 #ifdef UDE_PROFILE
     a.prof = g_prof_buffer ? g_prof_buffer + (size_t)PROF_FWD_SLOT * NPROF : nullptr;   // behind the backward's
 #endif
@@ -411,20 +441,25 @@ struct Ops {
     else if (ckpt) hipLaunchKernelGGL((ude_fwd_kernel<M, true>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     else hipLaunchKernelGGL((ude_fwd_kernel<M, false>), dim3(gf), dim3(NTHREADS), M::LDS_F, s, a);
     HIPCHK(hipGetLastError());
-    const double n_eval = 4.0 * (double)p->n_steps * (double)p->n_traj * (double)M::R;
-    hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, stats_out);
-    HIPCHK(hipGetLastError());
+    if (!ctl) {
+      hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, stats_slab, gf, n_eval, a.o_mean,
+                         a.o_std, a.o_norm);
+      HIPCHK(hipGetLastError());
+    }
     return UDE_OK;
   }
 
+  // st: the forward's statistics (read); dst: their cotangents (nullable); ctl: null = the separate
+  // tail launches (grad finalize, static partial / reduce, dy0 static), else the one tail kernel
   static int backward(const UdeProblem* p, const float* pack, const void* sched, const float* y0,
-                      const float* ckpt, const float* dlatent, const float* dlat_sir, const float* stats_out,
-                      const float* dstats, float* dy0, float* slab, float* dparams, hipStream_t s) {
+                      const float* ckpt, const float* dlatent, const float* dlat_sir, const UdeSideStats* st,
+                      const UdeSideStatsGrad* dst, float* dy0, float* slab, unsigned* ctl, float* dparams,
+                      hipStream_t s) {
     if constexpr (RC_VIEW) {
-      if (p->recompute) return Ops<Recompute<M>>::backward(p, pack, sched, y0, ckpt, dlatent, dlat_sir, stats_out,
-                                                           dstats, dy0, slab, dparams, s);
+      if (p->recompute) return Ops<Recompute<M>>::backward(p, pack, sched, y0, ckpt, dlatent, dlat_sir, st, dst,
+                                                           dy0, slab, ctl, dparams, s);
     }
-    if (!pack || !sched || !y0 || !stats_out || !dstats || !dy0 || !slab || !dparams) return UDE_E_INVALID;
+    if (!pack || !sched || !y0 || !stats_ok(st) || !dy0 || !slab || !dparams) return UDE_E_INVALID;
     if (p->n_steps > 0 && !ckpt) return UDE_E_INVALID;
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
@@ -435,7 +470,9 @@ struct Ops {
     KArgs a;
     memset(&a, 0, sizeof(a));
     a.pack = pack; a.y0 = y0; a.sched = (const unsigned char*)sched;
-    a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.dlat_sir = dlat_sir; a.stats_out = stats_out; a.dstats = dstats;
+    a.ckpt = (float*)ckpt; a.dlatent = dlatent; a.dlat_sir = dlat_sir;
+    a.st_mean = st->mean; a.st_std = st->std; a.st_norm = st->fa_norm;
+    if (dst) { a.d_mean = dst->d_mean; a.d_std = dst->d_std; a.d_norm = dst->d_fa_norm; }
     a.dy0 = dy0; a.slab = slab;
     if (M::BAYES) a.eslab = pack + (size_t)n_evals(p) * M::PACK_TOTAL;
     float* g0buf = slab + (size_t)gb * M::SLAB_STRIDE;
@@ -473,6 +510,13 @@ struct Ops {
     hipLaunchKernelGGL((ude_bwd_kernel<M>), dim3(gb), dim3(M::BWD_THREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
     HIPCHK(static_tsum(p, dlatent, dy0, s));
+    if (ctl) {
+      hipLaunchKernelGGL((ude_bwd_tail_kernel<M>), dim3(Tail<M>::blocks(n_tiles)), dim3(256), Tail<M>::LDS, s,
+                         (const float*)slab, gb, (const float*)g0buf, pack, y0, dlatent, p->n_traj, n_tiles,
+                         p->n_out + 1, part, ctl, dy0, dparams);
+      HIPCHK(hipGetLastError());
+      return UDE_OK;
+    }
     hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
                        (const float*)slab, gb, dparams);
     HIPCHK(hipGetLastError());
@@ -603,7 +647,7 @@ struct DopriOps {
     HIPCHK(hipGetLastError());
     const double n_eval = (double)h.n_evals * (double)p->n_traj * (double)M::R;
     hipLaunchKernelGGL(ude_stats_finalize_kernel<0>, dim3(1), dim3(320), 0, s, a.stats_slab, grid,
-                       n_eval, stats_out);
+                       n_eval, stats_out, stats_out + 2, stats_out + 4);
     HIPCHK(hipGetLastError());
     return UDE_OK;
   }
@@ -824,9 +868,11 @@ struct Entry {
   int (*pack)(const float* const*, const float* const*, float*, hipStream_t);
   int (*pack_bayes)(const UdeProblem*, const float* const*, const float* const*, const float* const*,
                     const float* const*, const float*, float*, hipStream_t);
-  int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*, float*, hipStream_t);
+  int (*forward)(const UdeProblem*, const float*, const void*, const float*, float*, float*, double*,
+                 const UdeSideStats*, unsigned*, hipStream_t);
   int (*backward)(const UdeProblem*, const float*, const void*, const float*, const float*, const float*,
-                  const float*, const float*, const float*, float*, float*, float*, hipStream_t);
+                  const float*, const UdeSideStats*, const UdeSideStatsGrad*, float*, float*, unsigned*, float*,
+                  hipStream_t);
   int (*dopri5_workspace)(const UdeProblem*, int, int64_t*);
   int (*dopri5_forward)(const UdeProblem*, const float*, const double*, double, double, double, int, const float*,
                         float*, void*, float*, UdeDopriInfo*, hipStream_t);
@@ -843,7 +889,7 @@ struct Entry {
                  void*, float*, hipStream_t);
   int (*dec_pack)(const float*, const float*, float*, hipStream_t);
   int (*forward_dec)(const UdeProblem*, const float*, const void*, const float*, const float*, float*, float*, double*,
-                     double*, float*, float*, hipStream_t);
+                     double*, const UdeSideStats*, unsigned*, float*, hipStream_t);
   int (*dec_backward)(const UdeProblem*, const void*, const float*, const float*, const float*, const float*, void*,
                       float*, float*, float*, hipStream_t);
   int (*nll_workspace)(int, int, int, int64_t*);

@@ -68,8 +68,13 @@ struct KArgs {
   float* ckpt;
   double* stats_slab;
   const float* dlatent;
-  const float* stats_out;
-  const float* dstats;
+  // side statistics of the solve (backward: read) and their cotangents (nullable: zero)
+  const float* st_mean;       // 2 floats: mean beta, mean gamma (posterior loc, lib/models.py:152-156)
+  const float* st_std;        // 2 floats: unbiased std (posterior scale)
+  const float* st_norm;       // 1 float: |Fa| (torch.norm(torch.stack(tracker)), lib/VAE.py:180)
+  const float* d_mean;
+  const float* d_std;
+  const float* d_norm;
   float* dy0;
   float* slab;
   int n_traj, n_steps, n_out, n_tiles;
@@ -84,6 +89,15 @@ struct KArgs {
   double* reg_slab;           // DEC forward: per-workgroup latent_init_loss partial sums
   float* ckpt_final;          // DEC training forward: the final-state block (ckpt + ckpt_final_off)
   float* gst;                 // GST backward: layer-output gradient rows [tile][step][stage][16][ACT_A4]
+  // forward: the statistics finalised in the kernel by its last workgroup (ctl != nullptr; the
+  // separate ude_stats_finalize_kernel otherwise)
+  unsigned int* ctl;          // arrival counter, zero on entry, left zero
+  float* o_mean;              // 2 floats
+  float* o_std;               // 2 floats
+  float* o_norm;              // 1 float
+  double* o_sums;             // 5 doubles: sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2 (nullable)
+  float* o_reg;               // DEC: latent_init_loss (1 float)
+  double n_eval;              // 4 n_steps N R: the number of recorded rates per statistic
 };
 
 // latent_init_loss summand (lib/train_functions.py:116-126): |x| where x < 0, |1 - x| where x > 1
@@ -600,6 +614,60 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Fixed-order sum of one statistic's per-workgroup partials by one wave (lane-strided, then a fixed
+// butterfly): the order of ude_stats_finalize_kernel / ude_sum_finalize_kernel, so both paths give the
+// same bits.  The partials are read with device-coherent loads (written by other workgroups, possibly
+// on other XCDs, with device-coherent stores).
+__device__ __forceinline__ double wave_sum_partials(const double* part, int n, int stride, int off, int ln) {
+  double s = 0.0;
+  for (int gi = ln; gi < n; gi += 64)
+    s += __hip_atomic_load(part + (size_t)gi * stride + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  return s;
+}
+
+// Statistics from the per-workgroup partials, by wave 0 of the last workgroup to arrive (ticket on
+// A.ctl):
+//   mean_c = S_c / n, std_c = sqrt((S2_c - n mean_c^2) / (n - 1)) (torch's unbiased std,
+//   lib/models.py:152-156), |Fa| = sqrt(S_Fa) (lib/VAE.py:180); DEC: latent_init_loss.
+// Publication without agent-scope fences: on gfx950 those write back / invalidate the whole L2 of the
+// XCD (buffer_wbl2 / buffer_inv sc1), which at the end of a forward that has just written GBs of
+// checkpoints cost 52 us per launch (measured).  Instead the partials go out as device-scope (sc1)
+// stores, complete (s_waitcnt vmcnt(0)) before the ticket is taken, and the last workgroup reads them
+// with device-scope loads: the device-coherent path, no cache maintenance.  The counter is reset for
+// the next launch (stream ordered).
+template <bool DEC>
+__device__ void finalize_stats_last(const KArgs& A, int ln) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): this wave's partial stores are complete
+  unsigned int ticket = 0;
+  if (ln == 0) ticket = __hip_atomic_fetch_add(A.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __builtin_amdgcn_readfirstlane(ticket);
+  if (ticket != gridDim.x - 1) return;
+  const int ng = gridDim.x;
+  double tot[5];
+#pragma unroll
+  for (int c = 0; c < 5; ++c) tot[c] = wave_sum_partials(A.stats_slab, ng, 5, c, ln);
+  double reg = 0.0;
+  if constexpr (DEC) reg = wave_sum_partials(A.reg_slab, ng, 1, 0, ln);
+  if (ln < 2) {
+    const double n = A.n_eval, t0 = ln == 0 ? tot[0] : tot[1], t2 = ln == 0 ? tot[2] : tot[3];
+    const double m = t0 / n;
+    const double var = (t2 - n * m * m) / (n - 1.0);
+    if (A.o_mean) A.o_mean[ln] = (float)m;
+    if (A.o_std) A.o_std[ln] = (float)sqrt(var > 0.0 ? var : 0.0);
+  }
+  if (ln == 2 && A.o_norm) A.o_norm[0] = (float)sqrt(tot[4]);
+  if (ln == 3 && DEC) A.o_reg[0] = (float)reg;
+  if (A.o_sums && ln < 5) {
+    double v = tot[0];
+#pragma unroll
+    for (int c = 1; c < 5; ++c) v = ln == c ? tot[c] : v;
+    A.o_sums[ln] = v;
+  }
+  if (ln == 0) *A.ctl = 0u;
+}
+
 // ============================================================================
 // Forward solve
 // ============================================================================
@@ -649,7 +717,15 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
-    float ys[SL][3], k1[SL][3], k2[SL][3], k3[SL][3];
+    // The RK4 state and the 3/8-rule combinations are carried in fp64 (the stage evaluations stay fp32:
+    // every stage input is rounded to fp32 for the MLPs, the checkpoint and the masks).  The reference's
+    // torchdiffeq combination runs in fp32; on trajectories that pass next to the mask boundary of
+    // lib/models.py:130 its rounding is amplified ~1e5-fold (whole-batch weight
+    // gradients of the M1 FaFp batch 5x outside the fp32 oracle's spread); an fp64 state brings those
+    // trajectories 2-50x closer to fp64 (tools/ns_traj.py, "fp32 rhs / fp64 state") at 3 extra VGPRs per
+    // state slot and a few fp64 VALU operations per stage.
+    double ys[SL][3];
+    float k1[SL][3], k2[SL][3], k3[SL][3];
     // DEC: y_hat of output jo from the state in the record's Y slot (decoder row tiles over the
     // waves; no barrier: the next write of the Y slot is behind the next stage's layer barriers)
     auto dec_emit = [&](int jo) {
@@ -691,10 +767,11 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
         const float* src = A.y0 + ((size_t)n * M::R + r) * M::L;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          ys[sl][c] = valid ? src[c] : 0.f;
-          lds[t * SR + M::Y_OFF + 3 * r + c] = ys[sl][c];
-          if (TRAIN && !CKR && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = ys[sl][c];
-          if (DEC && valid) *st_reg += (double)reg_term(ys[sl][c]);
+          const float y = valid ? src[c] : 0.f;
+          ys[sl][c] = (double)y;
+          lds[t * SR + M::Y_OFF + 3 * r + c] = y;
+          if (TRAIN && !CKR && A.n_steps > 0) A.ckpt[ckpt_index(tile, A.n_steps, 0, 0, M::F, 3 * r + c, t)] = y;
+          if (DEC && valid) *st_reg += (double)reg_term(y);
         }
         if (valid && !DEC && !rows16) {
           float* dst = A.latent + ((size_t)n * M::R + r) * M::L;
@@ -828,34 +905,45 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) f[c] = (Y[c] > 2.f || Y[c] < -1.f) ? 0.f : f[c];
             float Yn[3];
+            const double dd = (double)dt;
             if (j == 0) {
 #pragma unroll
-              for (int c = 0; c < 3; ++c) { k1[sl][c] = f[c]; Yn[c] = ys[sl][c] + (dt * f[c]) * (1.0f / 3.0f); }
+              for (int c = 0; c < 3; ++c) {
+                k1[sl][c] = f[c];
+                Yn[c] = (float)(ys[sl][c] + (dd * (double)f[c]) * (1.0 / 3.0));
+              }
             } else if (j == 1) {
 #pragma unroll
-              for (int c = 0; c < 3; ++c) { k2[sl][c] = f[c]; Yn[c] = ys[sl][c] + dt * (f[c] - k1[sl][c] * (1.0f / 3.0f)); }
+              for (int c = 0; c < 3; ++c) {
+                k2[sl][c] = f[c];
+                Yn[c] = (float)(ys[sl][c] + dd * ((double)f[c] - (double)k1[sl][c] * (1.0 / 3.0)));
+              }
             } else if (j == 2) {
 #pragma unroll
-              for (int c = 0; c < 3; ++c) { k3[sl][c] = f[c]; Yn[c] = ys[sl][c] + dt * ((k1[sl][c] - k2[sl][c]) + f[c]); }
+              for (int c = 0; c < 3; ++c) {
+                k3[sl][c] = f[c];
+                Yn[c] = (float)(ys[sl][c] + dd * (((double)k1[sl][c] - (double)k2[sl][c]) + (double)f[c]));
+              }
             } else {
               float yold[3];
 #pragma unroll
               for (int c = 0; c < 3; ++c) {
-                yold[c] = ys[sl][c];
-                const float dy = (((k1[sl][c] + 3.0f * (k2[sl][c] + k3[sl][c])) + f[c]) * dt) * 0.125f;
+                yold[c] = (float)ys[sl][c];
+                const double dy =
+                    ((((double)k1[sl][c] + 3.0 * ((double)k2[sl][c] + (double)k3[sl][c])) + (double)f[c]) * dd) * 0.125;
                 ys[sl][c] = ys[sl][c] + dy;
-                Yn[c] = ys[sl][c];
+                Yn[c] = (float)ys[sl][c];
               }
               if constexpr (DEC) {
                 // every output is a grid hit (mode 1): latent_init_loss of the new state; y_hat
                 // follows from the record after the barrier (dec_emit)
                 if (valid && sc.out_start[step] < sc.out_start[step + 1]) {
 #pragma unroll
-                  for (int c = 0; c < 3; ++c) *st_reg += (double)reg_term(ys[sl][c]);
+                  for (int c = 0; c < 3; ++c) *st_reg += (double)reg_term(Yn[c]);
                 }
                 if (TRAIN && step == A.n_steps - 1) {
 #pragma unroll
-                  for (int c = 0; c < 3; ++c) A.ckpt_final[((size_t)tile * M::F + 3 * r + c) * TT + t] = ys[sl][c];
+                  for (int c = 0; c < 3; ++c) A.ckpt_final[((size_t)tile * M::F + 3 * r + c) * TT + t] = Yn[c];
                 }
               } else if (valid && UDE_ABL != 16) {
                 const int o_end = sc.out_start[step + 1];
@@ -868,8 +956,8 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
                   for (int c = 0; c < 3; ++c) {
                     float v;
                     if (mode == 0) v = yold[c];
-                    else if (mode == 1) v = ys[sl][c];
-                    else v = yold[c] + slope * (ys[sl][c] - yold[c]);
+                    else if (mode == 1) v = Yn[c];
+                    else v = yold[c] + slope * (Yn[c] - yold[c]);
                     dst[c] = v;
                   }
                 }
@@ -912,9 +1000,15 @@ __device__ void fwd_body(const KArgs& A, float* lds) {
   if (tid < NS) {
     double s = 0;
     for (int w = 0; w < WAVES; ++w) s += red[w * NS + tid];
-    if (tid < 5) A.stats_slab[(size_t)blockIdx.x * 5 + tid] = s;
-    else A.reg_slab[blockIdx.x] = s;
+    double* dst = tid < 5 ? A.stats_slab + (size_t)blockIdx.x * 5 + tid : A.reg_slab + blockIdx.x;
+    // in-kernel finalize (ctl): device-coherent store, read back by the last workgroup (see
+    // finalize_stats_last)
+    if (A.ctl) __hip_atomic_store(dst, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *dst = s;
   }
+  // the last workgroup to finish turns every workgroup's partials into the statistics (no separate
+  // finalize launch; wave 0 only, so the split forward's partner waves keep their barrier sequence)
+  if (A.ctl && tid < 64) finalize_stats_last<DEC>(A, tid);
 #ifdef UDE_PROFILE
   if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)blockIdx.x * NPROF + i] = prof_.acc[i];
 #endif
@@ -1650,15 +1744,15 @@ __device__ void bwd_body(const KArgs& A, float* lds) {
   if constexpr (M::HAS_P) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      mu[c] = A.stats_out[c];
-      ca[c] = (float)((double)A.dstats[c] / nev);
-      const double sd = (double)A.stats_out[2 + c];
-      cb[c] = (float)((double)A.dstats[2 + c] / ((nev - 1.0) * sd));
+      mu[c] = A.st_mean[c];
+      ca[c] = A.d_mean ? (float)((double)A.d_mean[c] / nev) : 0.f;
+      const double sd = (double)A.st_std[c];
+      cb[c] = A.d_std ? (float)((double)A.d_std[c] / ((nev - 1.0) * sd)) : 0.f;
     }
   }
   if constexpr (M::HAS_A) {
-    const float nrm = A.stats_out[4];
-    cn = nrm > 0.f ? A.dstats[4] / nrm : 0.f;
+    const float nrm = A.st_norm[0];
+    cn = (nrm > 0.f && A.d_norm) ? A.d_norm[0] / nrm : 0.f;
   }
 
   // SPLITB: the weight-gradient accumulators live on the partner waves (bwd_wbody / bwd_wbody_l)
@@ -2677,11 +2771,10 @@ __device__ __forceinline__ int slab_to_param(int off) {
 // consecutive slab offsets (coalesced reads) x 4 groups of slabs, each summed in
 // slab order, then combined in a fixed order; the result is scattered to torch order.
 template <class M>
-__global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __restrict__ slab, int ngrid,
-                                                                float* __restrict__ dparams) {
-  __shared__ float part[4][64];
+__device__ __forceinline__ void grad_finalize_body(const float* __restrict__ slab, int ngrid, float* __restrict__ dparams,
+                                                   int blk, float (*part)[64]) {
   const int lo = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int off = blockIdx.x * 64 + lo;
+  const int off = blk * 64 + lo;
   float v = 0.f;
   if (off < M::SLAB_TOTAL) {
     const int per = (ngrid + 3) / 4, g0 = grp * per, g1 = min(ngrid, g0 + per);
@@ -2695,6 +2788,12 @@ __global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __r
     const int e = slab_to_param<M>(off);
     if (e >= 0) dparams[e] = (part[0][lo] + part[1][lo]) + (part[2][lo] + part[3][lo]);
   }
+}
+template <class M>
+__global__ __launch_bounds__(256) void ude_grad_finalize_kernel(const float* __restrict__ slab, int ngrid,
+                                                                float* __restrict__ dparams) {
+  __shared__ float part[4][64];
+  grad_finalize_body<M>(slab, ngrid, dparams, blockIdx.x, part);
 }
 
 // BAYES: the eps stream ([eval][N_PARAMS], torch order) re-laid out per evaluation in
@@ -2788,14 +2887,12 @@ __global__ __launch_bounds__(256) void ude_static_reduce_kernel(const float* __r
 // The time sums read the tile's contiguous (16, R, L) block of every output time
 // (coalesced, all dims) into LDS first: the static dims alone are a 5-of-8 stride.
 template <class M>
-__global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __restrict__ g0buf,
-                                                             const float* __restrict__ pack,
-                                                             const float* __restrict__ dlatent, int n_traj,
-                                                             int n_times, float* __restrict__ dy0) {
-  extern __shared__ float tsum[];                    // [TT][R][L] time sums of d latent
+__device__ __forceinline__ void dy0_static_body(const float* __restrict__ g0buf, const float* __restrict__ pack,
+                                                const float* __restrict__ dlatent, int n_traj, int n_times,
+                                                float* __restrict__ dy0, int tile, float* tsum) {
+  // tsum: [TT][R][L] time sums of d latent (LDS)
   constexpr int NST = M::S16 / 16, SPW = (NST + 3) / 4, BLK = TT * M::R * M::L;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
-  const int tile = blockIdx.x;
   const size_t NRL = (size_t)n_traj * M::R * M::L;
   if (!dlatent) {                                    // static cotangents all zero
     #pragma unroll 1
@@ -2870,6 +2967,165 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
     }
   }
 }
+template <class M>
+__global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __restrict__ g0buf,
+                                                             const float* __restrict__ pack,
+                                                             const float* __restrict__ dlatent, int n_traj,
+                                                             int n_times, float* __restrict__ dy0) {
+  extern __shared__ float tsum[];
+  dy0_static_body<M>(g0buf, pack, dlatent, n_traj, n_times, dy0, blockIdx.x, tsum);
+}
+
+// ---- the backward's tail in ONE launch ----------------------------------------
+// Three independent jobs, one block role each, run side by side instead of four launches in series:
+//   [0, n_tiles)                dy0 static of one trajectory tile (dy0_static_body: HBM-bound time sums
+//                               of d latent + G0^T W0SP on MFMA)
+//   [.., + TCH * NST)           static weight gradient dW0[:, static] = sum_n G0[n] x_static[n]^T:
+//                               block (chunk c, static column tile st), 4 waves over the chunk's tiles,
+//                               summed in LDS in wave order, the chunk partial written; the last chunk
+//                               block of column tile st to arrive (ticket on ctl[1 + st], agent-scope
+//                               release / acquire) sums the TCH partials in chunk order and scatters
+//                               them to torch order -- no separate reduce launch, deterministic
+//   [.., + ngf)                 the gradient slabs' fixed-order sum (grad_finalize_body; BAYES: both
+//                               halves)
+// ctl[1 ..] are zero on entry and left zero.
+constexpr int TCH = 32;                              // static-gradient chunks
+template <class M>
+struct Tail {
+  static constexpr int NST = M::S16 / 16, NOT = M::K0 / 16;
+  static constexpr int N_SP = M::HOIST ? TCH * NST : 0;
+  static constexpr int NGF = (M::SLAB_TOTAL + 63) / 64;
+  static constexpr int N_GF = NGF * (M::BAYES ? 2 : 1);
+  // dynamic LDS: the dy0 tile's time sums, or 3 waves' static-gradient partial tiles
+  static constexpr int LDS = cmax(M::HOIST ? TT * M::R * M::L * 4 : 0, 3 * NOT * 256 * 4 + 16);
+  static int blocks(int n_tiles) { return (M::HOIST ? n_tiles : 0) + N_SP + N_GF; }
+  // chunk partials [NST][TCH][NOT][64 lanes][4] (MFMA C order) behind the G0 sums
+  static constexpr int64_t part_floats() { return M::HOIST ? (int64_t)NST * TCH * NOT * 256 : 0; }
+};
+
+template <class M>
+__device__ void static_grad_chunk(const float* __restrict__ g0buf, const float* __restrict__ y0, int n_traj,
+                                  int n_tiles, float* __restrict__ part, unsigned int* ctl,
+                                  float* __restrict__ dparams, int c, int st, float* lds) {
+  constexpr int NOT = Tail<M>::NOT, NST = Tail<M>::NST;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int per = (n_tiles + TCH - 1) / TCH;
+  const int tb = c * per, te = min(n_tiles, tb + per);
+  const int s = st * 16 + t;
+  const int r = s / (M::L - 3), cc = s - r * (M::L - 3);
+  const bool s_ok = s < M::S;
+  f4 acc[NOT];
+#pragma unroll
+  for (int o = 0; o < NOT; ++o) acc[o] = f4zero();
+  #pragma unroll 2
+  for (int tile = tb + w; tile < te; tile += WAVES) {
+    f4 a[NOT];
+#pragma unroll
+    for (int o = 0; o < NOT; ++o)
+      a[o] = *reinterpret_cast<const f4*>(g0buf + ((size_t)tile * M::K0 + o * 16 + t) * TT + 4 * g);
+    float b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = tile * TT + 4 * g + q;
+      b[q] = (s_ok && n < n_traj) ? y0[((size_t)n * M::R + r) * M::L + 3 + cc] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 0; o < NOT; ++o) acc[o] = mfma4(a[o][q], b[q], acc[o]);
+  }
+  // the 4 waves' partial tiles summed in wave order (LDS), written as this chunk's partial
+  f4* red = reinterpret_cast<f4*>(lds);
+  if (w > 0) {
+#pragma unroll
+    for (int o = 0; o < NOT; ++o) red[((w - 1) * NOT + o) * 64 + lane] = acc[o];
+  }
+  __syncthreads();
+  unsigned int* flag = reinterpret_cast<unsigned int*>(lds) + 3 * NOT * 256;   // behind the partial tiles
+  if (w == 0) {
+    // device-coherent (sc1) stores, complete before the ticket (no agent-scope fence: see
+    // finalize_stats_last)
+    double* dst = reinterpret_cast<double*>(part + ((size_t)st * TCH + c) * NOT * 256);
+#pragma unroll
+    for (int o = 0; o < NOT; ++o) {
+      const f4 v = ((acc[o] + red[o * 64 + lane]) + red[(NOT + o) * 64 + lane]) + red[(2 * NOT + o) * 64 + lane];
+      __hip_atomic_store(dst + (o * 64 + lane) * 2, __builtin_bit_cast(double, __builtin_shufflevector(v, v, 0, 1)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dst + (o * 64 + lane) * 2 + 1, __builtin_bit_cast(double, __builtin_shufflevector(v, v, 2, 3)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    unsigned int ticket = 0;
+    if (lane == 0) ticket = __hip_atomic_fetch_add(ctl + 1 + st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) *flag = ticket;
+  }
+  __syncthreads();
+  if (*flag != TCH - 1) return;                      // block-uniform
+  // last chunk of column tile st: the TCH partials in chunk order (device-coherent loads); element
+  // (o, lane, e) is row o * 16 + 4 (lane / 16) + e, static column st * 16 + lane % 16
+  const double* src = reinterpret_cast<const double*>(part + (size_t)st * TCH * NOT * 256);
+  for (int i = threadIdx.x; i < NOT * 64; i += 256) {
+    f4 v = f4zero();
+    #pragma unroll 8
+    for (int ch = 0; ch < TCH; ++ch) {
+      const double* q = src + ((size_t)ch * NOT * 64 + i) * 2;
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 lo = __builtin_bit_cast(f2, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const f2 hi = __builtin_bit_cast(f2, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      const f4 u = {lo[0], lo[1], hi[0], hi[1]};
+      v += u;
+    }
+    const int o = i >> 6, ln = i & 63;
+    const int sc = st * 16 + (ln & 15);
+    if (sc >= M::S) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int om = o * 16 + 4 * (ln >> 4) + e;
+      int net = 0, oo = om;
+      if (!M::HAS_P || om >= (M::HAS_P ? M::kout(0, 0) : 0)) {
+        net = 1;
+        oo = om - (M::HAS_P ? M::kout(0, 0) : 0);
+      }
+      const int out = net == 0 ? M::out_dim(0, 0) : M::out_dim(1, 0);
+      if (oo < out) {
+        const int w0 = net == 0 ? M::param_w_off(0, 0) : M::param_w_off(1, 0);
+        dparams[w0 + (size_t)oo * M::R * M::L + static_col<M>(sc)] = v[e];
+      }
+    }
+  }
+  if (threadIdx.x == 0) ctl[1 + st] = 0u;
+  (void)NST;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void ude_bwd_tail_kernel(const float* __restrict__ slab, int ngrid,
+                                                           const float* __restrict__ g0buf,
+                                                           const float* __restrict__ pack,
+                                                           const float* __restrict__ y0,
+                                                           const float* __restrict__ dlatent, int n_traj,
+                                                           int n_tiles, int n_times, float* __restrict__ part,
+                                                           unsigned int* ctl, float* __restrict__ dy0,
+                                                           float* __restrict__ dparams) {
+  extern __shared__ __attribute__((aligned(16))) float tl[];
+  int b = blockIdx.x;
+  if constexpr (M::HOIST) {
+    if (b < n_tiles) {
+      dy0_static_body<M>(g0buf, pack, dlatent, n_traj, n_times, dy0, b, tl);
+      return;
+    }
+    b -= n_tiles;
+    if (b < Tail<M>::N_SP) {
+      static_grad_chunk<M>(g0buf, y0, n_traj, n_tiles, part, ctl, dparams, b % TCH, b / TCH, tl);
+      return;
+    }
+    b -= Tail<M>::N_SP;
+  }
+  float (*pp)[64] = reinterpret_cast<float (*)[64]>(tl);
+  if (M::BAYES && b >= Tail<M>::NGF)
+    grad_finalize_body<M>(slab + M::SLAB_TOTAL, ngrid, dparams + M::N_PARAMS, b - Tail<M>::NGF, pp);
+  else
+    grad_finalize_body<M>(slab, ngrid, dparams, b, pp);
+}
 
 // fixed-order sum of per-workgroup fp64 partials -> one float (latent_init_loss of the DEC forward)
 template <int V_ = 0>
@@ -2884,7 +3140,8 @@ __global__ void ude_sum_finalize_kernel(const double* __restrict__ part, int n, 
 
 template <int V_ = 0>
 __global__ void ude_stats_finalize_kernel(double* __restrict__ slab, int ngrid, double n_eval,
-                                          float* __restrict__ out) {
+                                          float* __restrict__ o_mean, float* __restrict__ o_std,
+                                          float* __restrict__ o_norm) {
   // ... and the fp64 totals back into slab[0..4] (read by the data-parallel statistics exchange)
   // wave c sums statistic c: lane-strided partials, then a fixed butterfly (deterministic)
   __shared__ double tot[5];
@@ -2901,10 +3158,10 @@ __global__ void ude_stats_finalize_kernel(double* __restrict__ slab, int ngrid, 
   if (c < 2) {
     const double m = tot[c] / n_eval;
     const double var = (tot[2 + c] - n_eval * m * m) / (n_eval - 1.0);
-    out[c] = (float)m;
-    out[2 + c] = (float)sqrt(var > 0.0 ? var : 0.0);
+    if (o_mean) o_mean[c] = (float)m;
+    if (o_std) o_std[c] = (float)sqrt(var > 0.0 ? var : 0.0);
   }
-  if (c == 4) out[4] = (float)sqrt(tot[4]);
+  if (c == 4 && o_norm) o_norm[0] = (float)sqrt(tot[4]);
   if (c < 5) slab[c] = tot[c];
 }
 

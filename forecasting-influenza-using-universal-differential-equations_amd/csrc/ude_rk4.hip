@@ -13,6 +13,15 @@
 using ude::Entry;
 
 namespace {
+// the legacy contiguous statistics vectors ({mean[2], std[2], |Fa|}) as UdeSideStats / UdeSideStatsGrad
+UdeSideStats stats_of(float* stats_out) {
+  UdeSideStats st = {stats_out, stats_out ? stats_out + 2 : nullptr, stats_out ? stats_out + 4 : nullptr, nullptr};
+  return st;
+}
+UdeSideStatsGrad dstats_of(const float* d) {
+  UdeSideStatsGrad g = {d, d ? d + 2 : nullptr, d ? d + 4 : nullptr};
+  return g;
+}
 const ude::Entry* find(const UdeModelDesc* m) {
   if (!m) return nullptr;
   for (int i = 0; i < ude::kNumEntries; ++i)
@@ -58,8 +67,18 @@ int ude_rk4_forward(const UdeModelDesc* m, const UdeProblem* p, const float* pac
                     ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
-  if (!p || p->n_traj < 1 || p->n_steps < 0) return UDE_E_INVALID;
-  return e->forward(p, pack, sched, y0, latent, ckpt, stats_slab, stats_out, (hipStream_t)stream);
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || !stats_out) return UDE_E_INVALID;
+  const UdeSideStats st = stats_of(stats_out);
+  return e->forward(p, pack, sched, y0, latent, ckpt, stats_slab, &st, nullptr, (hipStream_t)stream);
+}
+
+int ude_rk4_forward_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                       const float* y0, float* latent, float* ckpt, double* stats_slab, uint32_t* ctl,
+                       const UdeSideStats* stats, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || !ctl || !stats) return UDE_E_INVALID;
+  return e->forward(p, pack, sched, y0, latent, ckpt, stats_slab, stats, ctl, (hipStream_t)stream);
 }
 
 int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
@@ -67,8 +86,10 @@ int ude_rk4_backward(const UdeModelDesc* m, const UdeProblem* p, const float* pa
                      const float* dstats, float* dy0, float* grad_slab, float* dparams, ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
-  if (!p || p->n_traj < 1 || p->n_steps < 0 || !dlatent) return UDE_E_INVALID;
-  return e->backward(p, pack, sched, y0, ckpt, dlatent, nullptr, stats_out, dstats, dy0, grad_slab, dparams,
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || !dlatent || !stats_out || !dstats) return UDE_E_INVALID;
+  const UdeSideStats st = stats_of(const_cast<float*>(stats_out));
+  const UdeSideStatsGrad dst = dstats_of(dstats);
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, nullptr, &st, &dst, dy0, grad_slab, nullptr, dparams,
                      (hipStream_t)stream);
 }
 
@@ -78,8 +99,23 @@ int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float
                          ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
-  if (!p || p->n_traj < 1 || p->n_steps < 0 || (!dlatent) == (!dlatent_sir)) return UDE_E_INVALID;
-  return e->backward(p, pack, sched, y0, ckpt, dlatent, dlatent_sir, stats_out, dstats, dy0, grad_slab, dparams,
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || (!dlatent) == (!dlatent_sir) || !stats_out || !dstats)
+    return UDE_E_INVALID;
+  const UdeSideStats st = stats_of(const_cast<float*>(stats_out));
+  const UdeSideStatsGrad dst = dstats_of(dstats);
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, dlatent_sir, &st, &dst, dy0, grad_slab, nullptr, dparams,
+                     (hipStream_t)stream);
+}
+
+int ude_rk4_backward_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                        const float* y0, const float* ckpt, const float* dlatent, const float* dlatent_sir,
+                        const UdeSideStats* stats, const UdeSideStatsGrad* dstats, float* dy0, float* grad_slab,
+                        uint32_t* ctl, float* dparams, ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 0 || (!dlatent) == (!dlatent_sir) || !stats || !ctl)
+    return UDE_E_INVALID;
+  return e->backward(p, pack, sched, y0, ckpt, dlatent, dlatent_sir, stats, dstats, dy0, grad_slab, ctl, dparams,
                      (hipStream_t)stream);
 }
 
@@ -186,8 +222,20 @@ int ude_rk4_forward_dec(const UdeModelDesc* m, const UdeProblem* p, const float*
                         double* reg_slab, float* stats_out, float* reg_out, ude_stream_t stream) {
   const Entry* e = find(m);
   if (!e) return UDE_E_UNSUPPORTED;
-  if (!p || p->n_traj < 1 || p->n_steps < 1) return UDE_E_INVALID;
-  return e->forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, stats_out, reg_out,
+  if (!p || p->n_traj < 1 || p->n_steps < 1 || !stats_out) return UDE_E_INVALID;
+  const UdeSideStats st = stats_of(stats_out);
+  return e->forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, &st, nullptr, reg_out,
+                        (hipStream_t)stream);
+}
+
+int ude_rk4_forward_dec_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                           const float* y0, const float* dec_pack, float* yhat, float* ckpt, double* stats_slab,
+                           double* reg_slab, uint32_t* ctl, const UdeSideStats* stats, float* reg_out,
+                           ude_stream_t stream) {
+  const Entry* e = find(m);
+  if (!e) return UDE_E_UNSUPPORTED;
+  if (!p || p->n_traj < 1 || p->n_steps < 1 || !stats || !ctl) return UDE_E_INVALID;
+  return e->forward_dec(p, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, stats, ctl, reg_out,
                         (hipStream_t)stream);
 }
 

@@ -42,7 +42,8 @@ EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_
                     "ude_loss_head_backward", "ude_loss_head_backward_sir", "ude_rhs_workspace",
                     "ude_rhs_forward", "ude_rhs_vjp", "ude_pack_decoder", "ude_rk4_forward_dec",
                     "ude_decoder_backward", "ude_nll_workspace", "ude_nll_forward", "ude_nll_backward",
-                    "ude_rhs_eval_vjp", "ude_lincomb", "ude_scaled_sumsq", "ude_build_info")
+                    "ude_rhs_eval_vjp", "ude_lincomb", "ude_scaled_sumsq", "ude_build_info",
+                    "ude_rk4_forward_ex", "ude_rk4_forward_dec_ex", "ude_rk4_backward_ex")
 SUMSQ_WS = 1025          # doubles of ude_scaled_sumsq's output / workspace (UDE_SUMSQ_WS)
 
 
@@ -68,7 +69,18 @@ class UdeSizes(ctypes.Structure):
                 ("n_params", ctypes.c_int64), ("grid_fwd", ctypes.c_int32), ("grid_bwd", ctypes.c_int32),
                 ("lds_fwd", ctypes.c_int32), ("lds_bwd", ctypes.c_int32),
                 ("dec_pack_bytes", ctypes.c_int64), ("ckpt_final_bytes", ctypes.c_int64),
-                ("dec_ws_bytes", ctypes.c_int64), ("act_bytes", ctypes.c_int64)]
+                ("dec_ws_bytes", ctypes.c_int64), ("act_bytes", ctypes.c_int64), ("ctl_bytes", ctypes.c_int64)]
+
+
+class UdeSideStats(ctypes.Structure):
+    """mean (2) / std (2) / fa_norm (1) float buffers and the fp64 totals (5, nullable)."""
+    _fields_ = [("mean", ctypes.c_void_p), ("std", ctypes.c_void_p), ("fa_norm", ctypes.c_void_p),
+                ("sums", ctypes.c_void_p)]
+
+
+class UdeSideStatsGrad(ctypes.Structure):
+    """Cotangents of mean / std / fa_norm (each nullable: zero)."""
+    _fields_ = [("d_mean", ctypes.c_void_p), ("d_std", ctypes.c_void_p), ("d_fa_norm", ctypes.c_void_p)]
 
 
 def make_desc(cfg: _cfgs.Config) -> UdeModelDesc:
@@ -165,6 +177,13 @@ class NativeLib:
         L.ude_scaled_sumsq.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
+        pst, pdst = ctypes.POINTER(UdeSideStats), ctypes.POINTER(UdeSideStatsGrad)
+        L.ude_rk4_forward_ex.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, pst, vp]
+        L.ude_rk4_forward_ex.restype = i32
+        L.ude_rk4_forward_dec_ex.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, vp, vp, vp, pst, vp, vp]
+        L.ude_rk4_forward_dec_ex.restype = i32
+        L.ude_rk4_backward_ex.argtypes = [pdesc, pprob, vp, vp, vp, vp, vp, vp, pst, pdst, vp, vp, vp, vp, vp]
+        L.ude_rk4_backward_ex.restype = i32
 
     def supported(self, desc: UdeModelDesc) -> bool:
         return bool(self.lib.ude_supported(ctypes.byref(desc)))
@@ -202,6 +221,23 @@ class NativeLib:
         check(self.lib.ude_rk4_backward_sir(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
                                             dlat_sir, stats_out, dstats, dy0, slab, dparams, stream),
               "ude_rk4_backward_sir")
+
+    def forward_ex(self, desc, prob, pack, sched, y0, latent, ckpt, stats_slab, ctl, stats: UdeSideStats,
+                   stream) -> None:
+        check(self.lib.ude_rk4_forward_ex(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, latent, ckpt,
+                                          stats_slab, ctl, ctypes.byref(stats), stream), "ude_rk4_forward_ex")
+
+    def forward_dec_ex(self, desc, prob, pack, sched, y0, dec_pack, yhat, ckpt, stats_slab, reg_slab, ctl,
+                       stats: UdeSideStats, reg_out, stream) -> None:
+        check(self.lib.ude_rk4_forward_dec_ex(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, dec_pack,
+                                              yhat, ckpt, stats_slab, reg_slab, ctl, ctypes.byref(stats), reg_out,
+                                              stream), "ude_rk4_forward_dec_ex")
+
+    def backward_ex(self, desc, prob, pack, sched, y0, ckpt, dlatent, dlat_sir, stats: UdeSideStats,
+                    dstats: UdeSideStatsGrad, dy0, slab, ctl, dparams, stream) -> None:
+        check(self.lib.ude_rk4_backward_ex(ctypes.byref(desc), ctypes.byref(prob), pack, sched, y0, ckpt, dlatent,
+                                           dlat_sir, ctypes.byref(stats), ctypes.byref(dstats), dy0, slab, ctl,
+                                           dparams, stream), "ude_rk4_backward_ex")
 
     def dopri5_workspace(self, desc, prob, device: int) -> int:
         out = ctypes.c_int64(0)

@@ -77,15 +77,15 @@ def solve_decode(ode, y0: torch.Tensor, t: torch.Tensor, step_size, linear: torc
         # every evaluation's weight sample (models_bayes.py:43-48) from the solve's eps stream
         mus, sds = ode.ude_mean_std()
         eps = ode.take_eps(4 * plan.prob.n_steps, sum(int(p.numel()) for p in mus), y0.device)
-        yhat, reg, stats, token, ckpt, sums = _fused.FusedBayesRK4Dec.apply(
+        yhat, reg, mean, std, fa_norm, token, ckpt, sums = _fused.FusedBayesRK4Dec.apply(
             plan, y0.contiguous(), eps, linear.weight, linear.bias, *(mus + sds))
     else:
         params = []
         for lin in ode.ude_linears():
             params += [lin.weight, lin.bias]
-        yhat, reg, stats, token, ckpt, sums = _fused.FusedRK4Dec.apply(plan, y0.contiguous(), linear.weight,
-                                                                      linear.bias, *params)
-    ode._record_fused(stats, plan.n_eval, sums=sums)
+        yhat, reg, mean, std, fa_norm, token, ckpt, sums = _fused.FusedRK4Dec.apply(
+            plan, y0.contiguous(), linear.weight, linear.bias, *params)
+    ode._record_fused((mean, std, fa_norm), plan.n_eval, sums=sums)
     return yhat, reg, LazyLatent(token, ckpt, y0, plan), plan
 
 

@@ -7,8 +7,8 @@ PyTorch only provides device memory and the current HIP stream here.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import List, Optional, Tuple
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -30,6 +30,13 @@ class Plan:
     out_k: Optional[List[int]] = None
     n_regions: int = 0
     latent_dim: int = 0
+    # control words of the *_ex calls, one zeroed buffer per stream (include/ude_rk4.h: zero on entry,
+    # left zero by every call; calls sharing one are stream ordered)
+    ctl: Dict[int, torch.Tensor] = field(default_factory=dict)
+    # packed weights of the last forward and the (storage, version) of every parameter they were
+    # packed from (``packed_weights``)
+    pack_key: Optional[tuple] = None
+    pack: Optional[torch.Tensor] = None
 
 
 # Stored-activation budget (bytes) of one training solve: above it the training forward stores only
@@ -102,6 +109,65 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def _ctl(plan: Plan, dev) -> torch.Tensor:
+    stream = _stream(dev)
+    c = plan.ctl.get(stream)
+    if c is None:
+        c = plan.ctl[stream] = torch.zeros(max(int(plan.sizes.ctl_bytes) // 4, 1), dtype=torch.int32, device=dev)
+    return c
+
+
+def _stats_out(dev):
+    """Fresh (mean (2), std (2), fa_norm (1)) outputs + fp64 totals (5) of one solve: separate tensors,
+    so posterior() and the tracker read them without a split (and their cotangents reach the kernel
+    without a concatenation); written by the forward kernel's last workgroup."""
+    mean = torch.empty(2, dtype=torch.float32, device=dev)
+    std = torch.empty(2, dtype=torch.float32, device=dev)
+    norm = torch.empty(1, dtype=torch.float32, device=dev)
+    sums = torch.empty(5, dtype=torch.float64, device=dev)
+    st = _native.UdeSideStats(mean.data_ptr(), std.data_ptr(), norm.data_ptr(), sums.data_ptr())
+    return (mean, std, norm), sums, st
+
+
+def _stats_in(stats) -> "_native.UdeSideStats":
+    return _native.UdeSideStats(stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), None)
+
+
+def _dstats(*grads):
+    """(UdeSideStatsGrad, the tensors it points into): absent / placeholder cotangents -> NULL."""
+    keep = []
+    for g in grads:
+        if g is None or _is_placeholder(g):
+            keep.append(None)
+        else:
+            keep.append(g.contiguous().to(torch.float32))
+    return _native.UdeSideStatsGrad(*[_ptr(g) for g in keep]), keep
+
+
+def packed_weights(plan: Plan, params, dev) -> torch.Tensor:
+    """The fragment-order pack of a deterministic model's weights, re-packed only when a parameter's
+    storage or version counter changed since the last pack of this plan (an optimizer step, or any
+    in-place update through the parameter, bumps it).  Like autograd's own saved-tensor check, an
+    in-place write through ``param.data`` is not seen by the version counter: call
+    ``invalidate_packs()`` after such an edit."""
+    key = tuple((p.data_ptr(), p._version) for p in params)
+    if plan.pack is not None and plan.pack_key == key:
+        return plan.pack
+    ws = [p.contiguous() for p in params[0::2]]
+    bs = [p.contiguous() for p in params[1::2]]
+    pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
+    plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), _stream(dev))
+    plan.pack_key, plan.pack = key, pack
+    return pack
+
+
+def invalidate_packs() -> None:
+    """Drop every cached weight pack (after editing parameters through ``.data``)."""
+    from . import solvers
+    for plan in list(solvers._PLAN_CACHE.values()):
+        plan.pack_key, plan.pack = None, None
+
+
 _ZEROS = {}
 
 
@@ -139,9 +205,11 @@ def sir_token_like(latent: torch.Tensor) -> torch.Tensor:
 
 
 class FusedRK4(torch.autograd.Function):
-    """Returns (latent, stats, ckpt, sir_token, sums); sums = the solve's fp64 totals
-    (``stat_sums`` makes them differentiable); ckpt (the stage inputs of every step) is only a
-    real output when keep_ckpt is set (materialised tracking), else an empty tensor; sir_token
+    """Returns (latent, mean, std, fa_norm, ckpt, sir_token, sums): mean / std (2 each) / fa_norm (1)
+    the solve's side statistics as separate differentiable outputs (posterior() and the tracker read
+    them as they are; their cotangents go to ude_rk4_backward_ex as three pointers); sums = the solve's
+    fp64 totals (``stat_sums`` makes them differentiable); ckpt (the stage inputs of every step) is only
+    a real output when keep_ckpt is set (materialised tracking), else an empty tensor; sir_token
     (``sir_token_like``) receives compact S, I, R cotangents."""
 
     @staticmethod
@@ -149,35 +217,32 @@ class FusedRK4(torch.autograd.Function):
         dev = y0.device
         stream = _stream(dev)
         sz = plan.sizes
-        ws = [p.contiguous() for p in params[0::2]]
-        bs = [p.contiguous() for p in params[1::2]]
-        pack = torch.empty(sz.pack_bytes // 4, dtype=torch.float32, device=dev)
-        plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
+        pack = packed_weights(plan, params, dev)
         latent = torch.empty((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         need_grad = any(ctx.needs_input_grad[1:])
         ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
             if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
-        stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        stats, sums, st = _stats_out(dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
-        plan.lib.forward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                         latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), stats.data_ptr(), stream)
+        plan.lib.forward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                            latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), _ctl(plan, dev).data_ptr(), st,
+                            stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
         ctx.plan = plan
         ctx.set_materialize_grads(False)
         if need_grad:
-            ctx.save_for_backward(y0, pack, ckpt, stats)
+            ctx.save_for_backward(y0, pack, ckpt, *stats)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
-        sums = stats_slab[:5]
         ctx.mark_non_differentiable(out_ck, sums)
-        return latent, stats, out_ck, sir_token_like(latent), sums
+        return (latent,) + stats + (out_ck, sir_token_like(latent), sums)
 
     @staticmethod
-    def backward(ctx, dlatent, dstats, _dckpt=None, dl3=None, _dsums=None):
+    def backward(ctx, dlatent, dmean, dstd, dnorm, _dckpt=None, dl3=None, _dsums=None):
         plan: Plan = ctx.plan
-        y0, pack, ckpt, stats = ctx.saved_tensors
+        y0, pack, ckpt, *stats = ctx.saved_tensors
         dev = y0.device
         stream = _stream(dev)
         if dl3 is not None and _is_placeholder(dl3):
@@ -194,15 +259,15 @@ class FusedRK4(torch.autograd.Function):
                 dlatent = dlatent.clone()
                 dlatent[..., :3] += dl3
                 dl3 = None
-        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+        dst, _keep = _dstats(dmean, dstd, dnorm)
         dy0 = torch.empty_like(y0)
         slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
         dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
-        plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                              ckpt.data_ptr(), _ptr(dlatent), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
-                              dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        plan.lib.backward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                             ckpt.data_ptr(), _ptr(dlatent), _ptr(dl3), _stats_in(stats), dst, dy0.data_ptr(),
+                             slab.data_ptr(), _ctl(plan, dev).data_ptr(), dparams.data_ptr(), stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         return (None, dy0, None) + tuple(_split(dparams, plan.param_shapes))
@@ -212,7 +277,7 @@ class FusedRK4Dec(torch.autograd.Function):
     """Training solve with the decoder epilogue (lib/VAE.py:138, :186): the
     forward kernel emits y_hat (T, N, R) = Decoder(latent[..., :3]) and reg =
     latent_init_loss(latent[..., :3]) at the output times and writes no latent.  Returns
-    (y_hat, reg, stats, latent_token, ckpt, sums): latent_token is a stride-0 (T, N, R, L) placeholder
+    (y_hat, reg, mean, std, fa_norm, latent_token, ckpt, sums): latent_token is a stride-0 (T, N, R, L) placeholder
     (``materialize_latent`` turns it into the real latent on demand, its cotangent flowing back
     through the token); ckpt is the training store the latent is rebuilt from.
     Backward: ude_decoder_backward (d y_hat, d reg -> the compact S, I, R cotangent, d W_dec,
@@ -221,24 +286,21 @@ class FusedRK4Dec(torch.autograd.Function):
     @staticmethod
     def forward(ctx, plan: Plan, y0: torch.Tensor, Wd: torch.Tensor, bd: torch.Tensor, *params: torch.Tensor):
         dev = y0.device
-        stream = _stream(dev)
-        ws = [p.contiguous() for p in params[0::2]]
-        bs = [p.contiguous() for p in params[1::2]]
-        pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
-        plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), stream)
+        pack = packed_weights(plan, params, dev)
         yhat, reg, stats, ckpt, sums = _dec_forward(plan, y0, pack, Wd, bd)
         ctx.plan = plan
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(y0, pack, ckpt, stats, Wd.contiguous())
+        ctx.save_for_backward(y0, pack, ckpt, Wd.contiguous(), *stats)
         ctx.mark_non_differentiable(ckpt, sums)
         token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
-        return yhat, reg[0], stats, token, ckpt, sums
+        return (yhat, reg[0]) + stats + (token, ckpt, sums)
 
     @staticmethod
-    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None, _dsums=None):
+    def backward(ctx, dyhat, dreg, dmean, dstd, dnorm, dlatent, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
-        y0, pack, ckpt, stats, Wd = ctx.saved_tensors
-        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent)
+        y0, pack, ckpt, Wd, *stats = ctx.saved_tensors
+        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, (dmean, dstd, dnorm),
+                                               dlatent)
         return (None, dy0, dWd, dbd) + tuple(_split(dparams, plan.param_shapes))
 
 
@@ -265,16 +327,18 @@ class FusedBayesRK4Dec(torch.autograd.Function):
         yhat, reg, stats, ckpt, sums = _dec_forward(plan, y0, pack, Wd, bd)
         ctx.plan = plan
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(y0, pack, ckpt, stats, Wd.contiguous(), *sds)
+        ctx.save_for_backward(y0, pack, ckpt, Wd.contiguous(), *stats, *sds)
         ctx.mark_non_differentiable(ckpt, sums)
         token = zero_grad_like(torch.empty((plan.n_times,) + tuple(y0.shape), device="meta"), dev)
-        return yhat, reg[0], stats, token, ckpt, sums
+        return (yhat, reg[0]) + stats + (token, ckpt, sums)
 
     @staticmethod
-    def backward(ctx, dyhat, dreg, dstats, dlatent, _dckpt=None, _dsums=None):
+    def backward(ctx, dyhat, dreg, dmean, dstd, dnorm, dlatent, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
-        y0, pack, ckpt, stats, Wd, *sds = ctx.saved_tensors
-        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent)
+        y0, pack, ckpt, Wd, *rest = ctx.saved_tensors
+        stats, sds = rest[:3], rest[3:]
+        dy0, dWd, dbd, dparams = _dec_backward(plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, (dmean, dstd, dnorm),
+                                               dlatent)
         n = plan.sizes.n_params // 2
         d_mu = _split(dparams[:n], plan.param_shapes)
         d_sd = _split(_d_std(dparams[n:], sds), plan.param_shapes)
@@ -294,16 +358,16 @@ def _dec_forward(plan: Plan, y0: torch.Tensor, pack: torch.Tensor, Wd: torch.Ten
     ckpt = torch.empty((sz.ckpt_bytes + sz.ckpt_final_bytes) // 4, dtype=torch.float32, device=dev)
     stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
     reg_slab = torch.empty(max(sz.grid_fwd, 1), dtype=torch.float64, device=dev)
-    stats = torch.zeros(5, dtype=torch.float32, device=dev)
-    reg = torch.zeros(1, dtype=torch.float32, device=dev)
+    stats, sums, st = _stats_out(dev)
+    reg = torch.empty(1, dtype=torch.float32, device=dev)
     if EVENTS is not None:
         e0 = _ev(dev); e0.record()
-    plan.lib.forward_dec(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                         dec_pack.data_ptr(), yhat.data_ptr(), ckpt.data_ptr(), stats_slab.data_ptr(),
-                         reg_slab.data_ptr(), stats.data_ptr(), reg.data_ptr(), stream)
+    plan.lib.forward_dec_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                            dec_pack.data_ptr(), yhat.data_ptr(), ckpt.data_ptr(), stats_slab.data_ptr(),
+                            reg_slab.data_ptr(), _ctl(plan, dev).data_ptr(), st, reg.data_ptr(), stream)
     if EVENTS is not None:
         e1 = _ev(dev); e1.record(); EVENTS.append(("fwd_dec", e0, e1))
-    return yhat, reg, stats, ckpt, stats_slab[:5]
+    return yhat, reg, stats, ckpt, sums
 
 
 def _dec_backward(plan: Plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dlatent):
@@ -334,15 +398,15 @@ def _dec_backward(plan: Plan, y0, pack, ckpt, stats, Wd, dyhat, dreg, dstats, dl
         full = dlatent.contiguous().to(torch.float32).clone()
         full[..., :3] += dl3
         dl3 = None
-    dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+    dst, _keep = _dstats(*dstats)
     dy0 = torch.empty_like(y0)
     slab = torch.empty(max(sz.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
     dparams = torch.empty(sz.n_params, dtype=torch.float32, device=dev)
     if EVENTS is not None:
         e0 = _ev(dev); e0.record()
-    plan.lib.backward_sir(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                          ckpt.data_ptr(), _ptr(full), _ptr(dl3), stats.data_ptr(), dstats.data_ptr(),
-                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+    plan.lib.backward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                         ckpt.data_ptr(), _ptr(full), _ptr(dl3), _stats_in(stats), dst, dy0.data_ptr(),
+                         slab.data_ptr(), _ctl(plan, dev).data_ptr(), dparams.data_ptr(), stream)
     if EVENTS is not None:
         e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
     return dy0, dWd, dbd, dparams
@@ -377,36 +441,42 @@ def materialize_latent(token: torch.Tensor, ckpt: torch.Tensor, y0: torch.Tensor
 
 
 class _StatSums(torch.autograd.Function):
-    """The fp64 totals (sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2) of one fused solve
-    (``ude_stats_finalize_kernel`` leaves them in the stats slab), differentiable through the
-    solve's ``stats`` output [mean(2), std(2), |Fa|]: the kernel backward applies, per recorded
-    rate p and A-net output a,  dmean / n + dstd (p - mean) / ((n - 1) std)  and  d|Fa| a / |Fa|;
-    the cotangent g of the sums needs  g1 + 2 g2 p  and  2 g4 a, i.e.
+    """The fp64 totals (sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2) of one fused solve,
+    differentiable through the solve's statistics outputs (mean (2), std (2), |Fa| (1)): the kernel
+    backward applies, per recorded rate p and A-net output a,  dmean / n + dstd (p - mean) / ((n - 1) std)
+    and  d|Fa| a / |Fa|; the cotangent g of the sums needs  g1 + 2 g2 p  and  2 g4 a, i.e.
       dmean = n (g1 + 2 g2 mean),  dstd = 2 g2 (n - 1) std,  d|Fa| = 2 g4 |Fa|.
     Used by the data-parallel exchange (all-reduce the kernel's fp64 sums, no
     re-expansion of fp32 mean / std)."""
 
     @staticmethod
-    def forward(ctx, stats: torch.Tensor, sums: torch.Tensor, n: float):
-        ctx.save_for_backward(stats)
+    def forward(ctx, mean: torch.Tensor, std: torch.Tensor, norm: torch.Tensor, sums: torch.Tensor, n: float):
+        ctx.save_for_backward(mean, std, norm)
         ctx.n = float(n)
         return sums.clone()
 
     @staticmethod
     def backward(ctx, g):
-        (stats,) = ctx.saved_tensors
+        mean, std, norm = ctx.saved_tensors
         n = ctx.n
-        st = stats.double()
         g = g.double()
-        d = torch.zeros(5, dtype=torch.float64, device=g.device)
-        d[0:2] = n * (g[0:2] + 2.0 * g[2:4] * st[0:2])
-        d[2:4] = 2.0 * g[2:4] * (n - 1.0) * st[2:4]
-        d[4] = 2.0 * g[4] * st[4]
-        return d.to(stats.dtype), None, None
+        dm = n * (g[0:2] + 2.0 * g[2:4] * mean.double())
+        ds = 2.0 * g[2:4] * (n - 1.0) * std.double()
+        dn = 2.0 * g[4:5] * norm.double()
+        return dm.to(mean.dtype), ds.to(std.dtype), dn.to(norm.dtype), None, None
 
 
-def stat_sums(stats: torch.Tensor, sums: torch.Tensor, n: float) -> torch.Tensor:
-    return _StatSums.apply(stats, sums, n)
+def split_stats(stats):
+    """(mean, std, |Fa|) of a solve: the fused solves' three outputs, or a legacy {mean[2], std[2],
+    |Fa|} vector (the dopri5 forward)."""
+    if isinstance(stats, (tuple, list)):
+        return tuple(stats)
+    return tuple(stats.split([2, 2, 1]))
+
+
+def stat_sums(stats, sums: torch.Tensor, n: float) -> torch.Tensor:
+    mean, std, norm = split_stats(stats)
+    return _StatSums.apply(mean, std, norm, sums, n)
 
 
 def _split(flat: torch.Tensor, shapes) -> List[torch.Tensor]:
@@ -427,7 +497,7 @@ class FusedBayesRK4(torch.autograd.Function):
 
     Inputs: plan, y0, eps, keep_ckpt, then the means (w, b per layer, torch order) and the raw
     stds in the same order.  The kernel returns d/d mean and d/d |std|; the sign of
-    std (torch's abs backward) is applied here.  Returns (latent, stats, ckpt, sums): ckpt is the
+    std (torch's abs backward) is applied here.  Returns (latent, mean, std, fa_norm, ckpt, sums): ckpt is the
     training store when keep_ckpt is set (materialised tracking), else an empty tensor."""
 
     @staticmethod
@@ -448,39 +518,41 @@ class FusedBayesRK4(torch.autograd.Function):
         ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
             if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
-        stats = torch.zeros(5, dtype=torch.float32, device=dev)
+        stats, sums, st = _stats_out(dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
-        plan.lib.forward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                         latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), stats.data_ptr(), stream)
+        plan.lib.forward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                            latent.data_ptr(), _ptr(ckpt), stats_slab.data_ptr(), _ctl(plan, dev).data_ptr(), st,
+                            stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("fwd", e0, e1))
         ctx.plan = plan
+        ctx.set_materialize_grads(False)
         if need_grad:
-            ctx.save_for_backward(y0, pack, ckpt, stats, *sds)
-        sums = stats_slab[:5]
+            ctx.save_for_backward(y0, pack, ckpt, *stats, *sds)
         out_ck = ckpt if keep_ckpt else torch.empty(0, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(out_ck, sums)
-        return latent, stats, out_ck, sums
+        return (latent,) + stats + (out_ck, sums)
 
     @staticmethod
-    def backward(ctx, dlatent, dstats, _dckpt=None, _dsums=None):
+    def backward(ctx, dlatent, dmean, dstd, dnorm, _dckpt=None, _dsums=None):
         plan: Plan = ctx.plan
-        y0, pack, ckpt, stats, *sds = ctx.saved_tensors
+        y0, pack, ckpt, *rest = ctx.saved_tensors
+        stats, sds = rest[:3], rest[3:]
         dev = y0.device
         stream = _stream(dev)
-        if dlatent is None:
+        if dlatent is None or _is_placeholder(dlatent):
             dlatent = torch.zeros((plan.n_times,) + tuple(y0.shape), dtype=torch.float32, device=dev)
         dlatent = dlatent.contiguous().to(torch.float32)
-        dstats = torch.zeros(5, dtype=torch.float32, device=dev) if dstats is None else dstats.contiguous().float()
+        dst, _keep = _dstats(dmean, dstd, dnorm)
         dy0 = torch.empty_like(y0)
         slab = torch.empty(max(plan.sizes.grad_slab_bytes // 4, 1), dtype=torch.float32, device=dev)
         dparams = torch.empty(plan.sizes.n_params, dtype=torch.float32, device=dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
-        plan.lib.backward(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
-                          _ptr(ckpt), dlatent.data_ptr(), stats.data_ptr(), dstats.data_ptr(),
-                          dy0.data_ptr(), slab.data_ptr(), dparams.data_ptr(), stream)
+        plan.lib.backward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
+                             _ptr(ckpt), dlatent.data_ptr(), None, _stats_in(stats), dst, dy0.data_ptr(),
+                             slab.data_ptr(), _ctl(plan, dev).data_ptr(), dparams.data_ptr(), stream)
         if EVENTS is not None:
             e1 = _ev(dev); e1.record(); EVENTS.append(("bwd", e0, e1))
         n = plan.sizes.n_params // 2

@@ -84,18 +84,59 @@ class _TrackerView(torch.autograd.Function):
     reference's only use (lib/VAE.py:180); other functions of the entries get that projection."""
 
     @staticmethod
-    def forward(ctx, stats, fa_all):
-        ctx.save_for_backward(stats, fa_all)
+    def forward(ctx, fa_norm, fa_all):
+        ctx.save_for_backward(fa_norm, fa_all)
         return fa_all.clone()
 
     @staticmethod
     def backward(ctx, g):
-        stats, fa_all = ctx.saved_tensors
-        nrm = stats[4]
-        d = torch.zeros_like(stats)
-        d[4] = torch.where(nrm > 0, (g.double() * fa_all.double()).sum() / nrm.double(),
-                           torch.zeros((), dtype=torch.float64, device=g.device)).to(stats.dtype)
-        return d, None
+        fa_norm, fa_all = ctx.saved_tensors
+        nrm = fa_norm.reshape(())
+        d = torch.where(nrm > 0, (g.double() * fa_all.double()).sum() / nrm.double(),
+                        torch.zeros((), dtype=torch.float64, device=g.device)).to(fa_norm.dtype)
+        return d.reshape(fa_norm.shape), None
+
+
+class _NormOfOne(torch.autograd.Function):
+    """torch.norm of one non-negative value (the solve's |Fa|): the value itself, as a view.  Its
+    cotangent goes back unchanged -- d|x|/dx = 1 for x > 0; at |Fa| = 0 the kernel ignores d|Fa|, as
+    torch's norm backward gives 0 there."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.view(ctx.shape)
+
+
+class FaNormEntry(torch.Tensor):
+    """``tracker`` entry of a fused solve: its |Fa| (one value, the norm of every A-net output of the
+    solve).  The reference reads the tracker as ``torch.norm(torch.stack(ode.tracker))`` (lib/VAE.py:180)
+    -- the norm of all entries together.  For a tracker of ONE such entry that expression is the entry
+    itself: stack is served as a view and the norm by ``_NormOfOne`` (no device operators, the
+    cotangent handed straight to the solve's d|Fa|).  Everything else -- several entries, other norms,
+    any other operator -- runs the stock operators on plain tensors."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is torch.stack and len(args) >= 1 and isinstance(args[0], (list, tuple)) and len(args[0]) == 1 \
+                and isinstance(args[0][0], FaNormEntry) and args[0][0].numel() == 1 and "out" not in kwargs:
+            dim = kwargs.get("dim", args[1] if len(args) > 1 else 0)
+            with torch._C.DisableTorchFunctionSubclass():
+                v = args[0][0].unsqueeze(dim)
+            return v.as_subclass(FaNormEntry)
+        if func in (torch.norm, torch.Tensor.norm, torch.linalg.vector_norm) and len(args) >= 1 \
+                and isinstance(args[0], FaNormEntry) and args[0].numel() == 1 and len(args) == 1 \
+                and all(kwargs.get(k) in (None, "fro", 2, 2.0) for k in ("p", "ord")) \
+                and all(kwargs.get(k) is None for k in ("dim", "dtype", "out")) and not kwargs.get("keepdim"):
+            with torch._C.DisableTorchFunctionSubclass():
+                return _NormOfOne.apply(args[0])
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
 
 
 class _UDEModule(nn.Module):
@@ -138,16 +179,17 @@ class _UDEModule(nn.Module):
         self.tracker = []
 
     # -- fused-solver side statistics ------------------------------------------
-    def _record_fused(self, stats: torch.Tensor, n_eval: int, evals=None, sums=None) -> None:
-        """stats = [mean_b, mean_g, std_b, std_g, |Fa|] from one fused solve; evals = the
-        materialised (rates (E, N, R, 2), Fa (E, N, R, 3)) of its evaluations, or None; sums = the
-        solve's fp64 totals (sum b, sum g, sum b^2, sum g^2, sum Fa^2), read by the data-parallel
-        statistics exchange (distributed.sync_side_stats)."""
+    def _record_fused(self, stats, n_eval: int, evals=None, sums=None) -> None:
+        """stats = (mean (2), std (2), |Fa| (1)) of one fused solve -- its three outputs (or a legacy
+        [mean_b, mean_g, std_b, std_g, |Fa|] vector); evals = the materialised (rates (E, N, R, 2),
+        Fa (E, N, R, 3)) of its evaluations, or None; sums = the solve's fp64 totals (sum b, sum g,
+        sum b^2, sum g^2, sum Fa^2), read by the data-parallel statistics exchange
+        (distributed.sync_side_stats).  The solve's outputs are used as they are: posterior() and the
+        tracker norm add no device operator between the solve and the loss."""
+        from .fused import split_stats
+        s_mean, s_std, s_fa = split_stats(stats)
         if sums is not None and evals is None:
-            self._fused_sums.append((float(n_eval), stats, sums))
-        # one split node: its backward concatenates the three cotangents into d stats (three slice
-        # nodes each zero-filled, copied and accumulated a 5-vector: eight small kernels per step)
-        s_mean, s_std, s_fa = stats.split([2, 2, 1])
+            self._fused_sums.append((float(n_eval), (s_mean, s_std, s_fa), sums))
         if self.ode_type in ("Fp", "FaFp"):
             self._fused_rates.append((float(n_eval), s_mean, s_std))
             if evals is not None:
@@ -158,11 +200,11 @@ class _UDEModule(nn.Module):
                 self.params.fused_ids.update(id(e) for e in entries)
         if self.ode_type in ("Fa", "FaFp"):
             if evals is not None:
-                self.tracker.extend(_TrackerView.apply(stats, evals[1]).unbind(0))
+                self.tracker.extend(_TrackerView.apply(s_fa, evals[1]).unbind(0))
             else:
                 # torch.norm(torch.stack(tracker)) over this entry == |Fa| of the solve,
                 # and over several entries == the norm of all of them together.
-                self.tracker.append(s_fa)
+                self.tracker.append(s_fa.as_subclass(FaNormEntry))
 
     @torch.no_grad()
     def _evals_from_checkpoint(self, ckpt: torch.Tensor, y0: torch.Tensor, n_steps: int, chunk: int = 64):

@@ -144,7 +144,9 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         n_par = sum(int(p.numel()) for p in mus)
         eps = func.take_eps(4 * plan.prob.n_steps, n_par, y0.device)
         keep = bool(func.materialize_tracking)
-        latent, stats, ckpt, sums = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, keep, *(mus + sds))
+        latent, mean, std, fa_norm, ckpt, sums = _fused.FusedBayesRK4.apply(plan, y0.contiguous(), eps, keep,
+                                                                            *(mus + sds))
+        stats = (mean, std, fa_norm)
         evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps, eps) if keep else None
         func._record_fused(stats, plan.n_eval, evals, sums=sums)
     else:
@@ -152,7 +154,9 @@ def fused_odeint(func: _UDEModule, y0: torch.Tensor, t: torch.Tensor, step_size=
         for lin in func.ude_linears():
             params += [lin.weight, lin.bias]
         keep = bool(func.materialize_tracking)
-        latent, stats, ckpt, sir_token, sums = _fused.FusedRK4.apply(plan, y0.contiguous(), keep, *params)
+        latent, mean, std, fa_norm, ckpt, sir_token, sums = _fused.FusedRK4.apply(plan, y0.contiguous(), keep,
+                                                                                  *params)
+        stats = (mean, std, fa_norm)
         latent._ude_sir_token = sir_token
         evals = func._evals_from_checkpoint(ckpt, y0, plan.prob.n_steps) if keep else None
         func._record_fused(stats, plan.n_eval, evals, sums=sums)

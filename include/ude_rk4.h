@@ -88,6 +88,7 @@ typedef struct UdeSizes {
   int64_t dec_ws_bytes;     /* ude_decoder_backward workspace                     */
   int64_t act_bytes;        /* part of ckpt_bytes holding stored activation rows
                                (0 with UdeProblem.recompute = 1)                 */
+  int64_t ctl_bytes;        /* control words of the *_ex calls (see below)         */
 } UdeSizes;
 
 /*
@@ -161,6 +162,51 @@ int ude_rk4_backward_sir(const UdeModelDesc* m, const UdeProblem* p, const float
                          const float* dlatent, const float* dlatent_sir, const float* stats_out,
                          const float* dstats, float* dy0, float* grad_slab, float* dparams,
                          ude_stream_t stream);
+
+/* ---- side statistics as separate buffers, statistics and gradients finalised in-kernel --------
+ * The reference reads a solve's statistics as three tensors: posterior() = Normal(mean, std) of every
+ * recorded rate (lib/models.py:152-156, lib/VAE.py:173) and torch.norm(torch.stack(tracker)) = |Fa|
+ * (lib/VAE.py:180).  The *_ex calls take them as separate device buffers (what the autograd layer
+ * hands over as three outputs / three cotangents: no split, concatenation or zero-fill between the
+ * solve and the loss), and finalise in the solve's own launches:
+ *   ude_rk4_forward_ex / ude_rk4_forward_dec_ex: the last workgroup of the forward kernel turns the
+ *     per-workgroup fp64 partials (stats_slab) into mean / std / |Fa| (and reg_out), in the fixed
+ *     order of the separate finalize kernel of ude_rk4_forward (same bits);
+ *   ude_rk4_backward_ex: the per-workgroup gradient slabs, the static-feature weight gradient and
+ *     dy0's static dims are formed by ONE trailing kernel (instead of four).
+ * ctl: ude_query's ctl_bytes of device memory, zeroed by the caller ONCE (e.g. at allocation) and
+ * left zero by every call; calls that share a ctl buffer must be stream ordered (one ctl per stream
+ * that runs solves concurrently).  Any UdeSideStats pointer of an absent net may be NULL; every
+ * UdeSideStatsGrad pointer is nullable (zero cotangent).  Results equal ude_rk4_forward /
+ * ude_rk4_backward_sir (statistics bitwise; the static-feature weight gradient within fp32 summation
+ * order). */
+typedef struct UdeSideStats {
+  float* mean;      /* 2 floats: mean beta, mean gamma        (posterior().loc)   */
+  float* std;       /* 2 floats: unbiased std of beta, gamma  (posterior().scale) */
+  float* fa_norm;   /* 1 float: |Fa| over every evaluation                         */
+  double* sums;     /* 5 doubles, nullable: sum beta, sum gamma, sum beta^2, sum gamma^2, sum Fa^2 */
+} UdeSideStats;
+
+typedef struct UdeSideStatsGrad {
+  const float* d_mean;     /* 2 floats, nullable */
+  const float* d_std;      /* 2 floats, nullable */
+  const float* d_fa_norm;  /* 1 float, nullable  */
+} UdeSideStatsGrad;
+
+int ude_rk4_forward_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                       const float* y0, float* latent, float* ckpt, double* stats_slab, uint32_t* ctl,
+                       const UdeSideStats* stats, ude_stream_t stream);
+
+int ude_rk4_forward_dec_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                           const float* y0, const float* dec_pack, float* yhat, float* ckpt, double* stats_slab,
+                           double* reg_slab, uint32_t* ctl, const UdeSideStats* stats, float* reg_out,
+                           ude_stream_t stream);
+
+/* stats: the forward's mean / std / fa_norm (read; sums unused). */
+int ude_rk4_backward_ex(const UdeModelDesc* m, const UdeProblem* p, const float* pack, const void* sched,
+                        const float* y0, const float* ckpt, const float* dlatent, const float* dlatent_sir,
+                        const UdeSideStats* stats, const UdeSideStatsGrad* dstats, float* dy0, float* grad_slab,
+                        uint32_t* ctl, float* dparams, ude_stream_t stream);
 
 /* ---- adaptive Dormand-Prince solve (forward) ---------------------------------
  * Replaces torchdiffeq.odeint(func, y0, t, rtol, atol, method='dopri5',

@@ -46,6 +46,9 @@ class OracleBayesRHS:
     n_calls: int = 0
     params: List[torch.Tensor] = field(default_factory=list)
     tracker: List[torch.Tensor] = field(default_factory=list)
+    # test instrumentation: "rev4" / "fwd4" sum every Linear's K products in blocks of 4, last / first
+    # block first (more samples of fp32 rounding, as OracleRHS.k_order)
+    k_order: str = "torch"
 
     def mu_sd(self):
         """(means, stds) in torch parameter order (rate net first)."""
@@ -87,11 +90,20 @@ class OracleBayesRHS:
             off += n
         return out, off
 
-    @staticmethod
-    def _mlp(h, wb):
+    def _linear(self, h, w, b):
+        if self.k_order not in ("rev4", "fwd4"):
+            return torch.nn.functional.linear(h, w, b)
+        K = h.shape[-1]
+        acc = b.expand(h.shape[:-1] + (w.shape[0],))
+        blocks = range(0, K, 4)
+        for k0 in (reversed(blocks) if self.k_order == "rev4" else blocks):
+            acc = acc + h[..., k0:k0 + 4] @ w[:, k0:k0 + 4].T
+        return acc
+
+    def _mlp(self, h, wb):
         k = len(wb) // 2
         for i in range(k):
-            h = torch.nn.functional.linear(h, wb[2 * i], wb[2 * i + 1])
+            h = self._linear(h, wb[2 * i], wb[2 * i + 1])
             if i < k - 2:
                 h = torch.nn.functional.elu(h)
         return h
@@ -165,4 +177,100 @@ def solve_and_grad_bayes(rhs: OracleBayesRHS, eps: torch.Tensor, y0: torch.Tenso
             fill = [torch.zeros_like(v) if gi is None else gi.detach() for gi, v in zip(g, [y0] + mu + sd)]
             out["grads"] = {"y0": fill[0], "mu": fill[1:1 + len(mu)], "sd": fill[1 + len(mu):]}
     rhs.clear_tracking()
+    return out
+
+
+def _bayes_chunk_stats(args):
+    """Pass 1 of ``solve_and_grad_bayes_chunked`` for one chunk: latent and fp64 side-statistic sums."""
+    rhs, eps, y0c, t, step_size, threads = args
+    if threads:
+        torch.set_num_threads(threads)
+    with torch.no_grad():
+        rhs.clear_tracking()
+        rhs.eps = eps
+        lat = odeint_rk4(rhs, y0c, t, step_size)
+        out = {"latent": lat}
+        if rhs.params:
+            p = torch.stack(rhs.params).reshape(-1, 2).double()
+            out["n"], out["s1"], out["s2"] = p.shape[0], p.sum(0), p.pow(2).sum(0)
+        if rhs.tracker:
+            out["sf"] = float(torch.stack(rhs.tracker).double().pow(2).sum())
+    rhs.clear_tracking()
+    return out
+
+
+def _bayes_chunk_grad(args):
+    """Pass 2: the chunk's share of the loss gradient (the side statistics held at their global
+    values, as oracle/ude_oracle.py _chunk_grad): d y0 of the chunk, d mean / d raw std of every layer."""
+    rhs, eps, y0c, t, step_size, dlc, dmean, dstd, dnorm, mean, std, norm, n, threads = args
+    if threads:
+        torch.set_num_threads(threads)
+    dt = y0c.dtype
+    mu, sd = rhs.mu_sd()
+    for w in mu + sd:
+        w.requires_grad_(True)
+    yc = y0c.detach().clone().requires_grad_(True)
+    rhs.clear_tracking()
+    rhs.eps = eps
+    lat = odeint_rk4(rhs, yc, t, step_size)
+    loss = (lat * dlc.to(dt)).sum()
+    if mean is not None and dmean is not None:
+        p = torch.stack(rhs.params).reshape(-1, 2)
+        m, s = mean.to(dt), std.to(dt)
+        loss = loss + (p.sum(0) * dmean.to(dt) / n).sum() \
+            + ((p - m).pow(2).sum(0) * dstd.to(dt) / (2.0 * (n - 1) * s)).sum()
+    if norm is not None and dnorm is not None and float(norm) > 0:
+        loss = loss + dnorm * torch.stack(rhs.tracker).pow(2).sum() / (2.0 * norm.to(dt))
+    g = torch.autograd.grad(loss, [yc] + mu + sd, allow_unused=True)
+    rhs.clear_tracking()
+    for w in mu + sd:
+        w.requires_grad_(False)
+    return [torch.zeros_like(v) if gi is None else gi.detach() for gi, v in zip(g, [yc] + mu + sd)]
+
+
+def solve_and_grad_bayes_chunked(rhs: OracleBayesRHS, eps: torch.Tensor, y0: torch.Tensor, t: torch.Tensor,
+                                 step_size, dlatent: Optional[torch.Tensor], dmean=None, dstd=None, dnorm=None,
+                                 chunk: int = 256, workers: int = 1):
+    """``solve_and_grad_bayes`` over trajectory chunks on ``workers`` spawned CPU processes (full-size
+    batches; every chunk draws the same eps rows -- a weight sample is shared by the whole batch within
+    one evaluation, models_bayes.py:43-48).  Exact: the side statistics couple the trajectories only
+    through their global values (pass 1), their gradient is linear in per-trajectory terms once those
+    are known (pass 2; oracle/ude_oracle.py solve_and_grad_chunked).  Returns dict(latent, mean, std,
+    fa_norm, grads = {y0, mu, sd})."""
+    import math
+    N = y0.shape[0]
+    dt = y0.dtype
+    starts = list(range(0, N, chunk))
+    threads = max(1, torch.get_num_threads() // workers) if workers > 1 else 0
+
+    def run(fn, jobs):
+        if workers <= 1:
+            return [fn(j) for j in jobs]
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+            return list(ex.map(fn, jobs))
+
+    rhs.clear_tracking()
+    st = run(_bayes_chunk_stats, [(rhs, eps, y0[c0:c0 + chunk], t, step_size, threads) for c0 in starts])
+    out = {"latent": torch.cat([s["latent"] for s in st], 1)}
+    mean = std = norm = None
+    n = 0
+    if "s1" in st[0]:
+        n = sum(s["n"] for s in st)
+        s1 = sum(s["s1"] for s in st)
+        s2 = sum(s["s2"] for s in st)
+        mean = s1 / n
+        std = torch.sqrt(torch.clamp(s2 - n * mean * mean, min=0.0) / (n - 1))
+        out["mean"], out["std"] = mean.to(dt), std.to(dt)
+    if "sf" in st[0]:
+        norm = torch.tensor(math.sqrt(sum(s["sf"] for s in st)), dtype=torch.float64)
+        out["fa_norm"] = norm.to(dt).reshape(1)
+    if dlatent is None:
+        return out
+    gl = run(_bayes_chunk_grad, [(rhs, eps, y0[c0:c0 + chunk], t, step_size, dlatent[:, c0:c0 + chunk], dmean, dstd,
+                                  dnorm, mean, std, norm, n, threads) for c0 in starts])
+    n_mu = len(rhs.mu_sd()[0])
+    acc = [sum(g[1 + i] for g in gl[1:]) + gl[0][1 + i] if len(gl) > 1 else gl[0][1 + i] for i in range(2 * n_mu)]
+    out["grads"] = {"y0": torch.cat([g[0] for g in gl], 0), "mu": acc[:n_mu], "sd": acc[n_mu:]}
     return out

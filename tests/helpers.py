@@ -50,10 +50,10 @@ def kernel_forward_masks(pkg, mod, y0, t, step_size, eps=None):
     with torch.no_grad():
         if mod.uncertainty == "bayes":          # eps: the solve's (4 n_steps, n_params) draw stream
             mus, sds = mod.ude_mean_std()
-            lat, _stats, ckpt, _sums = fused.FusedBayesRK4.apply(plan, yd, eps.to(dev), True, *(mus + sds))
+            lat, _m, _s, _n, ckpt, _sums = fused.FusedBayesRK4.apply(plan, yd, eps.to(dev), True, *(mus + sds))
         else:
             params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
-            lat, _stats, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
+            lat, _m, _s, _n, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
     mod.clear_tracking()
     N, R, _L = y0.shape
     tiles = (N + 15) // 16

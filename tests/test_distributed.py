@@ -103,3 +103,44 @@ def test_stat_sums_cotangent_maps_onto_the_kernel_inputs(pkg):
     fa.grad = None
     (torch.cat([p.sum(0), (p * p).sum(0), (fa * fa).sum().reshape(1)]) * g).sum().backward()
     assert torch.allclose(gp, p.grad) and torch.allclose(gf, fa.grad)
+
+
+def test_stat_sums_from_separate_outputs(pkg):
+    """The fused solves return (mean, std, |Fa|) as three outputs: stat_sums over them gives the same
+    totals and the same per-entry gradients as over the legacy 5-vector."""
+    from ude_amd.fused import stat_sums
+    gen = torch.Generator().manual_seed(4)
+    p = (torch.rand(40, 2, generator=gen, dtype=torch.float64) + 0.2).requires_grad_(True)
+    fa = torch.randn(40, 3, generator=gen, dtype=torch.float64).requires_grad_(True)
+    g = torch.randn(5, generator=gen, dtype=torch.float64)
+    raw = torch.cat([p.sum(0), (p * p).sum(0), (fa * fa).sum().reshape(1)]).detach()
+    (stat_sums((p.mean(0), p.std(0), torch.norm(fa).reshape(1)), raw, 40.0) * g).sum().backward()
+    g3 = (p.grad.clone(), fa.grad.clone())
+    p.grad = None
+    fa.grad = None
+    (stat_sums(torch.cat([p.mean(0), p.std(0), torch.norm(fa).reshape(1)]), raw, 40.0) * g).sum().backward()
+    assert torch.allclose(g3[0], p.grad) and torch.allclose(g3[1], fa.grad)
+
+
+def test_tracker_entry_norm_is_a_view(pkg):
+    """torch.norm(torch.stack(ode.tracker)) (lib/VAE.py:180) over the one |Fa|
+    entry a fused solve records is that entry (no device operator; its cotangent passes unchanged);
+    over several entries, or for other norms, the stock operators run."""
+    from ude_amd.rhs import FaNormEntry
+    src = torch.tensor([2.5], requires_grad=True)
+    e = (src * 1.0).as_subclass(FaNormEntry)
+    n = torch.norm(torch.stack([e]))
+    assert type(n) is torch.Tensor and n.shape == () and float(n.detach()) == 2.5
+    assert n.grad_fn is not None and "NormOfOne" in type(n.grad_fn).__name__
+    (3.0 * n).backward()
+    assert float(src.grad) == 3.0
+    # two entries: the norm of both, gradient x / |x|
+    src.grad = None
+    e = (src * 1.0).as_subclass(FaNormEntry)
+    e2 = (src * 2.0).as_subclass(FaNormEntry)
+    n2 = torch.norm(torch.stack([e, e2]))
+    assert abs(float(n2) - (2.5 ** 2 + 5.0 ** 2) ** 0.5) < 1e-6 and type(n2) is torch.Tensor
+    n2.backward()
+    assert abs(float(src.grad) - (2.5 * 1 + 5.0 * 2) / float(n2)) < 1e-6
+    # other operators: plain tensors out
+    assert type(e + 1) is torch.Tensor and float(torch.norm(torch.stack([e]), p=1)) == 2.5

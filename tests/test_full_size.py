@@ -18,10 +18,11 @@ import pytest
 import torch
 
 from helpers import EvalMaskRecorder, agreeing_trajectories, kernel_forward_masks, normwise_rel
-from oracle.ude_oracle_bayes import OracleBayesRHS, solve_and_grad_bayes
+from oracle.ude_oracle_bayes import OracleBayesRHS, solve_and_grad_bayes, solve_and_grad_bayes_chunked
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+WORKERS = int(os.environ.get("UDE_ORACLE_WORKERS", "12"))
 DM = torch.tensor([0.3, -0.2], dtype=torch.float64)
 DS = torch.tensor([0.5, 0.1], dtype=torch.float64)
 DN = 0.1
@@ -94,7 +95,25 @@ def _bayes_pair(pkg, mod, y0, t, h, eps, dl):
     return fused, per, errs, agreeing_trajectories(mf, mp), rec.margin, kink
 
 
-@pytest.mark.timeout(900)
+def _bayes_oracle_whole(mod, eps, y0, t, h, dl, dtype, k_order="torch"):
+    """The chunked Bayes oracle over the whole batch in ``dtype`` (the same loss as _loss_and_grads)."""
+    rhs = OracleBayesRHS.from_module(mod, dtype)
+    rhs.k_order = k_order
+    r = solve_and_grad_bayes_chunked(rhs, eps.to(dtype), y0.to(dtype), t, h, dl.to(dtype), DM.to(dtype),
+                                     DS.to(dtype), DN, chunk=512, workers=WORKERS)
+    return {"latent": r["latent"], "mean": r["mean"], "std": r["std"], "fa_norm": r["fa_norm"],
+            "y0": r["grads"]["y0"], "mu": r["grads"]["mu"], "sd": r["grads"]["sd"]}
+
+
+def _bayes_errs(a, b):
+    e = {k: normwise_rel(a[k], b[k]) for k in ("latent", "mean", "std", "fa_norm", "y0")}
+    for k in ("mu", "sd"):
+        for i, (x, y) in enumerate(zip(a[k], b[k])):
+            e[f"{k}{i}"] = normwise_rel(x, y)
+    return e
+
+
+@pytest.mark.timeout(2400)
 def test_bayes_state49_full_batch(pkg):
     """Trajectories whose evaluations take different mask decisions in the two paths (rounding next
     to the boundary of lib/models.py:130's mask) follow different branches of the RHS: the rows are
@@ -111,6 +130,27 @@ def test_bayes_state49_full_batch(pkg):
     assert pkg.fusable(mod, y0.to(DEV))
     fused, per, errs, agree, margin, kink = _bayes_pair(pkg, mod, y0, t, h, eps, dl)
     K = int(agree.sum())
+    # the WHOLE batch (near-kink and near-boundary trajectories included) against the
+    # fp64 Bayes oracle, chunked over CPU workers; the bars are the reference arithmetic's own spread: three
+    # fp32 runs of the oracle (torch's summation order, k_order "rev4" and "fwd4" -- the last is the order of
+    # the kernel's MFMA K chains) -- every quantity within max(floor, 2 x the farthest one), floors 1e-5
+    # (latent / statistics), 2e-5 (dy0), 5e-5 (d mean / d std)
+    mod.cpu()
+    dlc = dl.cpu().double()
+    r64 = _bayes_oracle_whole(mod, eps.double(), y0, t, h, dlc, torch.float64)
+    s32 = [_bayes_errs(_bayes_oracle_whole(mod, eps, y0, t, h, dlc, torch.float32, ko), r64)
+           for ko in ("torch", "rev4", "fwd4")]
+    ek = _bayes_errs(fused, r64)
+    mod.to(DEV)
+    bad = []
+    for k, v in ek.items():
+        floor = 1e-5 if k in ("latent", "mean", "std", "fa_norm") else (2e-5 if k == "y0" else 5e-5)
+        bar = max(floor, 2.0 * max(s[k] for s in s32))
+        if v > bar:
+            bad.append((k, v, bar))
+    print("bayes_state49 whole batch vs fp64 Bayes oracle [fp32 oracle torch / rev4 / fwd4 order]: "
+          + ", ".join(f"{k} {v:.2e} [{s32[0][k]:.1e}/{s32[1][k]:.1e}/{s32[2][k]:.1e}]" for k, v in ek.items()))
+    assert not bad, bad
     far = agree & (margin > 1e-3) & (kink > 1e-6)
     rows = {"latent": normwise_rel(fused["latent"][:, agree], per["latent"][:, agree]),
             "y0": normwise_rel(fused["y0"][agree], per["y0"][agree]),

@@ -160,9 +160,15 @@ def one_step(pkg, udist, mod, y0, t, dlat, world):
     if mod.ode_type in ("Fa", "FaFp"):
         outs.append(torch.norm(torch.stack(mod.tracker)))
         cots.append(_cot(0.1, y0.device))
+    if world > 1 and getattr(mod, "_ude_reducer", None) is None:
+        # the gradient all-reduce issued from autograd hooks as soon as the solve's backward has
+        # written the gradients, on a side stream (ude_amd.distributed.GradReducer)
+        mod._ude_reducer = udist.GradReducer(mod.parameters())
+    if world > 1:
+        mod._ude_reducer.arm()
     torch.autograd.backward(outs, cots)
     if world > 1:
-        udist.all_reduce_grads(mod.parameters())
+        mod._ude_reducer.finish()
 
 
 def time_steps(pkg, udist, mod, y0, t, dlat, world, steps, warmup, barrier, dev):
@@ -220,26 +226,6 @@ def cpu_baseline(w, mod_gpu, budget_s=10.0, threads=1):
                       f"the reference runs 1 thread, run_ode.py:28) on {n} trajectories x {len(tt) - 1} steps of "
                       f"the same model, fwd+bwd incl. posterior/|Fa| terms, best of {reps}",
             "host_cpus_visible": os.cpu_count()}
-
-
-def cpu_baseline_child(workload, threads, timeout_s=45):
-    """cpu_baseline at `threads` threads in a child process with a time cap (oversubscribing the
-    host share can stall for minutes): the same sample and weights (seed 0) as the main baselines."""
-    import subprocess
-    code = ("import sys, json, torch; sys.path.insert(0, %r); import bench, importlib; "
-            "pkg = importlib.import_module(bench.PKG); w = bench.WORKLOADS[%r]; "
-            "m, _, _, _ = bench.build(pkg, w, torch.device('cpu'), seed=1000); "
-            "print(json.dumps(bench.cpu_baseline(w, m, budget_s=5.0, threads=%d)))" % (REPO, workload, threads))
-    print(f"[bench] cpu baseline at {threads} threads (child, cap {timeout_s} s)", file=sys.stderr, flush=True)
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS=str(threads))
-    try:
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout_s, env=env)
-        return json.loads(r.stdout.strip().splitlines()[-1])
-    except subprocess.TimeoutExpired:
-        return {"value": None, "cores": threads, "note": f"not finished within {timeout_s} s: {threads} threads "
-                "oversubscribe this box's CPU share (OMP_NUM_THREADS=%s)" % os.environ.get("OMP_NUM_THREADS")}
-    except Exception as e:  # pragma: no cover
-        return {"value": None, "cores": threads, "note": f"failed: {e!r}"}
 
 
 def dopri5_line(pkg, w, dev, reps=3):
@@ -649,10 +635,7 @@ def main():
             m_cpu, _, _, _ = build(pkg, wm, torch.device("cpu"), seed=1000)
             res[name] = {"workload": wl, "threads_16": cpu_baseline(wm, m_cpu, threads=CPU_THREADS),
                          "threads_1": cpu_baseline(wm, m_cpu, threads=1)}
-        if (os.cpu_count() or 1) > CPU_THREADS:
-            # also at more host cores than this box's share per GPU (capped at 64 threads:
-            # at every visible core, 256 here, the shared host stalls for minutes)
-            res["cpu_baseline_many_cores"] = cpu_baseline_child(args.workload, min(os.cpu_count(), 64))
+        # (the box's usable host share is OMP_NUM_THREADS = 16 per GPU: no line above it -- VERDICT r4 item 8)
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

@@ -638,7 +638,7 @@ __device__ __forceinline__ double wave_sum_partials(const double* part, int n, i
 // with device-scope loads: the device-coherent path, no cache maintenance.  The counter is reset for
 // the next launch (stream ordered).
 template <bool DEC>
-__device__ void finalize_stats_last(const KArgs& A, int ln) {
+__device__ __forceinline__ void finalize_stats_last(const KArgs& A, int ln) {
   __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): this wave's partial stores are complete
   unsigned int ticket = 0;
   if (ln == 0) ticket = __hip_atomic_fetch_add(A.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2978,9 +2978,7 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
 
 // ---- the backward's tail in ONE launch ----------------------------------------
 // Three independent jobs, one block role each, run side by side instead of four launches in series:
-//   [0, n_tiles)                dy0 static of one trajectory tile (dy0_static_body: HBM-bound time sums
-//                               of d latent + G0^T W0SP on MFMA)
-//   [.., + TCH * NST)           static weight gradient dW0[:, static] = sum_n G0[n] x_static[n]^T:
+//   [0, TCH * NST)              static weight gradient dW0[:, static] = sum_n G0[n] x_static[n]^T:
 //                               block (chunk c, static column tile st), 4 waves over the chunk's tiles,
 //                               summed in LDS in wave order, the chunk partial written; the last chunk
 //                               block of column tile st to arrive (ticket on ctl[1 + st], agent-scope
@@ -2988,7 +2986,10 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
 //                               them to torch order -- no separate reduce launch, deterministic
 //   [.., + ngf)                 the gradient slabs' fixed-order sum (grad_finalize_body; BAYES: both
 //                               halves)
-// ctl[1 ..] are zero on entry and left zero.
+//   [.., + n_tiles)             dy0 static of one trajectory tile (dy0_static_body: HBM-bound time sums
+//                               of d latent + G0^T W0SP on MFMA)
+// The latency-bound chunk blocks are dispatched first (blocks start in index order), the bandwidth-bound
+// dy0 blocks fill the chip behind them.  ctl[1 ..] are zero on entry and left zero.
 constexpr int TCH = 32;                              // static-gradient chunks
 template <class M>
 struct Tail {
@@ -3109,22 +3110,21 @@ __global__ __launch_bounds__(256) void ude_bwd_tail_kernel(const float* __restri
   extern __shared__ __attribute__((aligned(16))) float tl[];
   int b = blockIdx.x;
   if constexpr (M::HOIST) {
-    if (b < n_tiles) {
-      dy0_static_body<M>(g0buf, pack, dlatent, n_traj, n_times, dy0, b, tl);
-      return;
-    }
-    b -= n_tiles;
     if (b < Tail<M>::N_SP) {
       static_grad_chunk<M>(g0buf, y0, n_traj, n_tiles, part, ctl, dparams, b % TCH, b / TCH, tl);
       return;
     }
     b -= Tail<M>::N_SP;
   }
-  float (*pp)[64] = reinterpret_cast<float (*)[64]>(tl);
-  if (M::BAYES && b >= Tail<M>::NGF)
-    grad_finalize_body<M>(slab + M::SLAB_TOTAL, ngrid, dparams + M::N_PARAMS, b - Tail<M>::NGF, pp);
-  else
-    grad_finalize_body<M>(slab, ngrid, dparams, b, pp);
+  if (b < Tail<M>::N_GF) {
+    float (*pp)[64] = reinterpret_cast<float (*)[64]>(tl);
+    if (M::BAYES && b >= Tail<M>::NGF)
+      grad_finalize_body<M>(slab + M::SLAB_TOTAL, ngrid, dparams + M::N_PARAMS, b - Tail<M>::NGF, pp);
+    else
+      grad_finalize_body<M>(slab, ngrid, dparams, b, pp);
+    return;
+  }
+  if constexpr (M::HOIST) dy0_static_body<M>(g0buf, pack, dlatent, n_traj, n_times, dy0, b - Tail<M>::N_GF, tl);
 }
 
 // fixed-order sum of per-workgroup fp64 partials -> one float (latent_init_loss of the DEC forward)

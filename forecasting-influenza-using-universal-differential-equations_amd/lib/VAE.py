@@ -322,10 +322,14 @@ class VAE:
                 loss, data, names = self.calc_loss(y_pred, y[lo:hi][:, eval_pts, :], losses=losses)
             finally:
                 self._dp_w = None
+            if "reducer" not in self._dp:
+                self._dp["reducer"] = udist.GradReducer(self.parameters(), average=False, group=self._dp["group"])
+            self._dp["reducer"].arm()
             loss.backward()
-            # one bucket: encoder + ODE + decoder gradients summed over the ranks (ref :205 then
-            # sees the global gradient on every rank: same gate, same Adam step)
-            udist.all_reduce_grads(self.parameters(), average=False, group=self._dp["group"])
+            # encoder + ODE + decoder gradients summed over the ranks, each bucket's all-reduce issued
+            # during the backward as soon as its gradients exist (ref :205 then sees the global
+            # gradient on every rank: same gate, same Adam step)
+            self._dp["reducer"].finish()
         else:
             y_pred = self(x, t[eval_pts], n_samples=n_samples, training=True)
             loss, data, names = self.calc_loss(y_pred, y[:, eval_pts, :], losses=losses)

@@ -76,19 +76,19 @@ class OracleRHS:
     record_masks: bool = False
     masks: List[torch.Tensor] = field(default_factory=list)
     margins: List[torch.Tensor] = field(default_factory=list)     # per evaluation: (N,) distance to the boundary
-    # test instrumentation: "rev4" sums every Linear's K products in blocks of 4, last block first, "fwd4"
-    # in blocks of 4 first block first (the order of an MFMA K chain) -- the same fp32 arithmetic with
-    # other summation orders (more samples of fp32 rounding)
+    # test instrumentation: "rev<k>" (k = 2, 4, 8, 16 ...) sums every Linear's K products in blocks of k,
+    # last block first, "fwd<k>" first block first (fwd4: the order of an MFMA K chain) -- the same fp32
+    # arithmetic with other summation orders (more samples of fp32 rounding)
     k_order: str = "torch"
 
     def _linear(self, h, w, b):
-        if self.k_order not in ("rev4", "fwd4"):
+        if self.k_order[:3] not in ("rev", "fwd"):
             return torch.nn.functional.linear(h, w, b)
-        K = h.shape[-1]
+        K, kb = h.shape[-1], int(self.k_order[3:])
         acc = b.expand(h.shape[:-1] + (w.shape[0],))
-        blocks = range(0, K, 4)
-        for k0 in (reversed(blocks) if self.k_order == "rev4" else blocks):
-            acc = acc + h[..., k0:k0 + 4] @ w[:, k0:k0 + 4].T
+        blocks = range(0, K, kb)
+        for k0 in (reversed(blocks) if self.k_order.startswith("rev") else blocks):
+            acc = acc + h[..., k0:k0 + kb] @ w[:, k0:k0 + kb].T
         return acc
 
     def _mlp(self, h, ws, bs, acts):

@@ -91,13 +91,13 @@ class OracleBayesRHS:
         return out, off
 
     def _linear(self, h, w, b):
-        if self.k_order not in ("rev4", "fwd4"):
+        if self.k_order[:3] not in ("rev", "fwd"):
             return torch.nn.functional.linear(h, w, b)
-        K = h.shape[-1]
+        K, kb = h.shape[-1], int(self.k_order[3:])
         acc = b.expand(h.shape[:-1] + (w.shape[0],))
-        blocks = range(0, K, 4)
-        for k0 in (reversed(blocks) if self.k_order == "rev4" else blocks):
-            acc = acc + h[..., k0:k0 + 4] @ w[:, k0:k0 + 4].T
+        blocks = range(0, K, kb)
+        for k0 in (reversed(blocks) if self.k_order.startswith("rev") else blocks):
+            acc = acc + h[..., k0:k0 + kb] @ w[:, k0:k0 + kb].T
         return acc
 
     def _mlp(self, h, wb):

@@ -317,10 +317,7 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
         }
         f4 r = gv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-        }
+        for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
         if (t16 == 0) {
           float* db = lds + M::DB_LDS + k * 16 + g * 4;
           db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];

@@ -116,7 +116,7 @@ __device__ __forceinline__ float reg_term(float v) {
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.
-constexpr int NPROF = 20;
+constexpr int NPROF = 28;
 constexpr int PROF_FWD_SLOT = 4096;          // the training forward's rows start at workgroup slot 4096
 struct Prof {
   unsigned long long acc[NPROF];
@@ -136,6 +136,23 @@ struct Prof {
 #else
 #define UDE_STAMP(pf, seg) do { } while (0)
 #endif
+
+// Sum over the 16 lanes of a DPP row -- the 16 trajectories t = lane & 15 of a tile row -- by four
+// DPP adds (quad_perm lane ^ 1, lane ^ 2, row_half_mirror, row_mirror): the association of the xor
+// butterfly, so bitwise the same sums, without the LDS-crossbar ds_bpermute round trips of
+// __shfl_xor (4 dependent LDS latencies per reduction).  Every lane of the row holds the sum.
+// (state49 bwd 1.83 -> 1.72 ms, gradients bit-identical: profiles/r05/ab_dpp.txt)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);      // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);      // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);     // row_half_mirror
+  v += dpp_mov<0x140>(v);     // row_mirror
+  return v;
+}
 
 // The step / output schedule (dt, the output CSR) is read every stage.  It is wave-uniform and
 // read-only, so it is read through the constant address space: scalar loads (s_load, scalar
@@ -1135,6 +1152,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
   float* rec = lds + t * SR;
   sfor<M::D>([&](auto ee) {
     constexpr int d = M::D - 1 - decltype(ee)::value;
+    UDE_STAMP(pf, 24 + d);
     // input-gradient fragments go out first; the LDS-only dW GEMMs below hide them
     constexpr int NX = M::XQ(W, d);
     f4 fx[(NX > 0 && !RW && !PF) ? NX : 1];
@@ -1207,10 +1225,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
           } else {
             f4 r = gvv[o];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-              r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-            }
+            for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
             if (t == 0) {
               float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
               db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
@@ -1235,10 +1250,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
           // wave's rows of the workgroup's LDS row sums (fixed order: deterministic)
           f4 r = gv;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-            r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-          }
+          for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
           if (t == 0) {
             float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
             db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
@@ -1394,6 +1406,7 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
         }
       }
     });
+    UDE_STAMP(pf, 20 + d);
     lds_sync();
     UDE_STAMP(pf, 7 + d);
   });
@@ -1690,10 +1703,7 @@ __device__ __forceinline__ void g0_tile_end(const KArgs& A, float* lds, const f4
       }
       f4 r = gv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-        r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-      }
+      for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
       if (t16 == 0) {
         float* db = lds + M::DB_LDS + k * 16 + g * 4;
         db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
@@ -2366,10 +2376,7 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
       if constexpr (M::fowner(d, k) == W) {
         f4 r = gacc[M::ng_before(W, d, k)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-          r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-        }
+        for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
         if (t16 == 0) {
           float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
           db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
@@ -2454,7 +2461,8 @@ __device__ __forceinline__ void dma_ckpt(const KArgs& A, float* lds, int tile, i
 // operands read in chunks of XC column tiles (registers: the dW accumulators fill this wave) and the
 // bias sums reduced across the tile's trajectories into the LDS row sums every phase.
 template <class M, int W, int SR, class After>
-__device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, int lane, const After& after) {
+__device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, int lane, const After& after,
+                                                  Prof* pf = nullptr) {
   const int t = lane & 15, g = lane >> 4;
   const float* rec = lds + t * SR;
   constexpr int XC = 4;
@@ -2491,10 +2499,7 @@ __device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, i
         } else {
           f4 r = gv;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r[e] += __shfl_xor(r[e], 1, 64); r[e] += __shfl_xor(r[e], 2, 64);
-            r[e] += __shfl_xor(r[e], 4, 64); r[e] += __shfl_xor(r[e], 8, 64);
-          }
+          for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
           if (t == 0) {
             float* db = lds + M::DB_LDS + (M::FTbase(d) + k) * 16 + g * 4;
             db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
@@ -2502,8 +2507,14 @@ __device__ __forceinline__ void mlp_backward_dw_l(float* lds, f4* dw, f4* g0t, i
         }
       }
     });
+    // the next stage's rows freed by phase d + 1 (D: the flux pass) are fetched behind this phase's
+    // MFMAs instead of ahead of them, except layer 0's (needed soonest: issued as phase 0 starts)
+    if constexpr (d + 1 >= 2) after(std::integral_constant<int, d + 1>{});
+    UDE_STAMP(pf, 20 + d);
     lds_sync_dma();
-    after(std::integral_constant<int, d>{});
+    UDE_STAMP(pf, 7 + d);
+    if constexpr (d == 1) after(std::integral_constant<int, 1>{});
+    UDE_STAMP(pf, 24 + d);
   });
 }
 
@@ -2519,6 +2530,15 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
   f4 dw[NDWn], g0t[NZn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  Prof prof_, *pf = nullptr;
+#ifdef UDE_PROFILE
+  // diagnostic: partner wave 4 (W = 0) stamps its own segments into row 2 * PROF_FWD_SLOT + block
+  if (W == 0 && A.prof && lane == 0) {
+    pf = &prof_;
+    for (int i = 0; i < NPROF; ++i) prof_.acc[i] = 0;
+    prof_.last = __builtin_amdgcn_s_memtime();
+  }
+#endif
   lds_sync();                                           // record zeroed
   // staged stage input [f][t] -> Y slot [t][f]: each wave moves exactly the 256-float chunks its own
   // dma_ckpt wrote (its vmcnt wait covers only its own DMAs; the other waves' may still be landing)
@@ -2556,28 +2576,38 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
         // operand reads) are recomputed here instead of hoisted out of the loop, where they spilled
         // next to the 176 dW VGPRs and every scratch reload (a vmcnt wait) drained the DMAs in flight
         asm volatile("" : "+v"(lane));
+        UDE_STAMP(pf, 13);
         wait_dma();                                     // this stage's rows and input have landed
+        UDE_STAMP(pf, 0);
         put_stage();
+        UDE_STAMP(pf, 2);
         lds_sync_dma();                                 // stage input + activation rows in the record
+        UDE_STAMP(pf, 1);
         if (have) dma_ckpt<M, W>(A, lds, tile, nstep, njj, lane);   // staging slot free again
+        UDE_STAMP(pf, 3);
         lds_sync_dma();                                 // flux pass: final-layer gradients written
-        if (have) dma_freed<M, W, M::D>(act_rsrc<M>(A, tile, nstep, njj), lds, lane);
+        UDE_STAMP(pf, 16);
+        UDE_STAMP(pf, 17);
         mlp_backward_dw_l<M, W, SR>(lds, dw, g0t, lane, [&](auto dd) {
           constexpr int d = decltype(dd)::value;
           if constexpr (d >= 1)
             if (have) dma_freed<M, W, d>(act_rsrc<M>(A, tile, nstep, njj), lds, lane);
-        });
+        }, pf);
       }
     }
     lds_sync_dma();                                     // tile end: dy0
     lds_sync_dma();
     g0_tile_end<M, W>(A, lds, g0t, tile, lane);
     lds_sync_dma();
+    UDE_STAMP(pf, 15);
   }
   wait_dma();
   f4 none[1];
   dw_to_slab<M, W>(dw, none, myslab, lane);
   lds_sync();                                           // bias row sums complete -> bwd_body copies them
+#ifdef UDE_PROFILE
+  if (pf) for (int i = 0; i < NPROF; ++i) A.prof[(size_t)(2 * PROF_FWD_SLOT + blockIdx.x) * NPROF + i] = prof_.acc[i];
+#endif
 }
 
 template <class M>

@@ -216,8 +216,9 @@ struct Model {
   // Large records (STORE_ACT_D) split the same way (SPLIT_BWD_L): waves 4-7 (bwd_wbody_l) hold the
   // weight-gradient accumulators (the ~176 VGPRs per wave that kept the 4-wave kernel at one wave per
   // SIMD) and move the next stage's data with LDS-DMA (global_load_lds): each layer's activation rows
-  // as soon as the current stage's last reader of that layer is past its barrier, and the checkpointed
-  // stage input into the staging slot -- no data registers, no exposed load at the stage start.
+  // once the current stage's last reader of that layer is past its barrier (issued behind the next
+  // phase's MFMAs), and the checkpointed stage input into the staging slot -- no data registers, no
+  // exposed load at the stage start.
 #ifndef UDE_NO_SPLIT_L
   static constexpr bool SPLIT_BWD_L = STORE_ACT_D && !BAYES;
 #else

@@ -2,7 +2,9 @@
 cuda:0 -- the 1-GPU test box) each solve half of the trajectories with the fused
 kernel; the side statistics are combined with ude_amd.distributed and the
 parameter gradients summed.  Must equal the single-process solve of the whole
-batch (same loss: data term + global posterior / |Fa| terms once)."""
+batch (same loss: data term + global posterior / |Fa| terms once).  The gradients are summed by
+GradReducer (bucket all-reduces issued during the backward on a side stream) in the "stats" case and
+by the one-shot all_reduce_grads in the "materialized" one."""
 import os
 import sys
 
@@ -55,9 +57,16 @@ def _worker(rank, port, q, materialize):
         dev = torch.device("cuda", 0)
         mod, y0, t, dl = _setup(pkg, dev, materialize)
         lo, hi = (0, 40) if rank == 0 else (40, N)          # uneven shards
+        red = None if materialize else udist.GradReducer(mod.parameters(), average=False, bucket_bytes=64 << 10)
+        if red is not None:
+            red.arm()
         loss, m, s, nrm = _loss(pkg, mod, y0[lo:hi].contiguous(), t, dl[:, lo:hi].contiguous(), WORLD)
         loss.backward()
-        udist.all_reduce_grads(mod.parameters(), average=False)
+        if red is not None:
+            # the overlapped path: bucket all-reduces issued from the gradient hooks on a side stream
+            red.finish()
+        else:
+            udist.all_reduce_grads(mod.parameters(), average=False)
         q.put((rank, m.cpu().numpy(), s.cpu().numpy(), nrm.cpu().numpy(), [p.grad.cpu().numpy() for p in mod.parameters()]))
         dist.barrier()
         dist.destroy_process_group()

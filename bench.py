@@ -584,7 +584,9 @@ def main():
                        "aug_net_sizes": w["aug"], "traj_per_gpu": per_rank, "global_batch": world * per_rank,
                        "rk4_steps": n_steps_rk, "parallelism": f"dp{world}",
                        "device": "cpu-rehearsal" if args.rehearse_cpu else "MI355X"},
-            "roofline": {"kernel": "ude_bwd_kernel (+ grad finalize)", "bound": "mfma",
+            # avg_launch_ms: HIP events on the launch stream around one ude_rk4_backward_ex call = the
+            # ude_bwd_kernel launch and its ude_bwd_tail_kernel (rocprof lists the two separately)
+            "roofline": {"kernel": "ude_bwd_kernel + ude_bwd_tail_kernel", "bound": "mfma",
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
                          "traffic": pmc, "traffic_source": PMC_SOURCE.get(args.workload + "_bwd"),

@@ -2531,8 +2531,10 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
   Prof prof_, *pf = nullptr;
-#ifdef UDE_PROFILE
-  // diagnostic: partner wave 4 (W = 0) stamps its own segments into row 2 * PROF_FWD_SLOT + block
+#if defined(UDE_PROFILE) && defined(UDE_PROFILE_PARTNER)
+  // diagnostic (-DUDE_PROFILE_PARTNER on top of -DUDE_PROFILE): partner wave 4 (W = 0) stamps its own
+  // segments into row 2 * PROF_FWD_SLOT + block.  Its stamps perturb the stage far more than the
+  // critical path's (s_memtime waits on the partner's LDS traffic): a separate build, for its shares.
   if (W == 0 && A.prof && lane == 0) {
     pf = &prof_;
     for (int i = 0; i < NPROF; ++i) prof_.acc[i] = 0;

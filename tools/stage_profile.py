@@ -43,12 +43,16 @@ PORDER = [15, 13, 0, 2, 1, 3, 16, 17, 23, 10, 27, 22, 9, 26, 21, 8, 25, 20, 7, 2
 
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "state49"      # [--build]: compile only (on the host)
+    # [--partner]: the partner-wave stamps too (a separate library)
     w = bench.WORKLOADS[wl]
     kind = "B" + w["kind"][len("Bayes_"):] if w["kind"].startswith("Bayes_") else w["kind"]
     cfg = (kind, w["R"], w["L"], tuple(w["net"]) if w["net"] else None, tuple(w["aug"]) if w["aug"] else None)
-    path = os.path.join(_native.BUILD, f"libude_rk4_profile_{wl}.so")
+    partner = "--partner" in sys.argv         # also stamp the SPLIT_BWD_L partner wave 4 (perturbs more)
+    path = os.path.join(_native.BUILD, f"libude_rk4_profile_{wl}{'_partner' if partner else ''}.so")
     if "--build" in sys.argv or not os.path.exists(path):
-        _native.build_library([cfg], path, "profile_" + wl, jobs=1, extra_flags=["-DUDE_PROFILE"])
+        flags = ["-DUDE_PROFILE"] + (["-DUDE_PROFILE_PARTNER"] if partner else [])
+        _native.build_library([cfg], path, "profile_" + wl + ("_partner" if partner else ""), jobs=1,
+                              extra_flags=flags)
         if "--build" in sys.argv:
             print("built", path)
             return

@@ -508,7 +508,9 @@ __device__ __forceinline__ void load_static(const float* __restrict__ y0, float*
 // load issued behind pending stores waits for them to complete).
 template <class M, int SR, int XOFF>
 __device__ __forceinline__ void fwd_tile_static(const KArgs& A, float* lds, int n0) {
-  constexpr int PS = (TT * M::S16 + NTHREADS - 1) / NTHREADS, CS = 4;
+  // every load of the thread in flight at once (state49: 16; 4 at a time measured fwd 0.921 -> 0.909 ms
+  // against this, profiles/r05/ab_tile_static.txt)
+  constexpr int PS = (TT * M::S16 + NTHREADS - 1) / NTHREADS, CS = PS < 16 ? PS : 16;
   int tid = threadIdx.x;
   // thread-derived offsets formed here each tile, not hoisted into registers the stage loop needs
   asm volatile("" : "+v"(tid));

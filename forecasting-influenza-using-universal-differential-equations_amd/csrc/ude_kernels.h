@@ -2290,6 +2290,7 @@ __device__ void bwd_wbody(const KArgs& A, float* lds) {
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
 #pragma unroll
   for (int i = 0; i < NGn; ++i) gacc[i] = f4zero();
+  __builtin_amdgcn_s_setprio(1);         // as bwd_wbody_l (M1 bwd 4.44 -> 4.38 ms, profiles/r05/ab_partner_prio_m1.txt)
   lds_sync();                            // record zeroed
   // These waves also move the stage data (the critical-path waves issue no global load in the
   // stage loop): each stage's checkpointed input and activation rows, loaded one stage ahead into
@@ -2532,6 +2533,10 @@ __device__ void bwd_wbody_l(const KArgs& A, float* lds) {
   f4 dw[NDWn], g0t[NZn];
 #pragma unroll
   for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  // the second-dispatched half of the workgroup at static priority 1 for the whole launch (the
+  // arbitration loser otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4): state49 bwd
+  // 1.744 -> 1.724 ms (profiles/r05/ab_partner_prio.txt)
+  __builtin_amdgcn_s_setprio(1);
   Prof prof_, *pf = nullptr;
 #if defined(UDE_PROFILE) && defined(UDE_PROFILE_PARTNER)
   // diagnostic (-DUDE_PROFILE_PARTNER on top of -DUDE_PROFILE): partner wave 4 (W = 0) stamps its own

@@ -3029,7 +3029,10 @@ __global__ __launch_bounds__(256) void ude_dy0_static_kernel(const float* __rest
 //                               of d latent + G0^T W0SP on MFMA)
 // The latency-bound chunk blocks are dispatched first (blocks start in index order), the bandwidth-bound
 // dy0 blocks fill the chip behind them.  ctl[1 ..] are zero on entry and left zero.
-constexpr int TCH = 32;                              // static-gradient chunks
+// static-gradient chunks: fewer, longer chunks win -- the last block's fixed-order sum of the chunk
+// partials (device-coherent loads) is the tail's long pole (state49 bwd + tail 1.719 / 1.686 / 1.692 ms
+// at 32 / 16 / 8 chunks, 1.737 / 1.810 at 64 / 128: profiles/r05/ab_tch_*.txt)
+constexpr int TCH = 16;
 template <class M>
 struct Tail {
   static constexpr int NST = M::S16 / 16, NOT = M::K0 / 16;

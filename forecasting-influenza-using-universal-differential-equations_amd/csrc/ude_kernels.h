@@ -110,9 +110,11 @@ __device__ __forceinline__ float reg_term(float v) {
 #ifndef UDE_ABL
 #define UDE_ABL 0
 #endif
-// Measured-off A/B variants of rounds 3-4 (two interleaved accumulation chains, early activation-row
-// stores, row-mapped latent outputs, raised critical-path priority) were
-// removed from the tree: profiles/r04/ab_*.log hold their measurements.
+// Measured-off A/B variants of rounds 3-5 (two interleaved accumulation chains, early activation-row
+// stores, row-mapped latent outputs, raised critical-path priority; round 5: input-gradient fragments
+// a phase earlier, interleaved static hoist, tail time sums with fewer round trips, forward copy-wave
+// priority, more static-gradient chunks) were removed from the tree: profiles/r04/ab_*.log and
+// profiles/r05/ab_*.txt hold their measurements.
 
 // In-kernel cycle stamps for a diagnostic build (-DUDE_PROFILE): wave-uniform
 // s_memtime deltas accumulated per segment; compiled out otherwise.

@@ -658,13 +658,32 @@ __device__ __forceinline__ double wave_sum_partials(const double* part, int n, i
 // stores, complete (s_waitcnt vmcnt(0)) before the ticket is taken, and the last workgroup reads them
 // with device-scope loads: the device-coherent path, no cache maintenance.  The counter is reset for
 // the next launch (stream ordered).
+//
+// Ordering argument (the atomics are relaxed: under the HIP/C++ memory model alone this pattern would
+// be a data race, so it rests on gfx950's hardware ordering, made explicit here):
+//  1. the partials are agent-scope (sc1) stores: written through to the device-coherent level, not
+//     left in a non-coherent cache;
+//  2. publish_fence(): s_waitcnt vmcnt(0) -- every store of the wave has been acknowledged (is visible
+//     device-wide) -- plus a compiler barrier, so no memory operation is moved across it;
+//  3. only then the ticket's agent-scope fetch_add (performed at the device-coherent level, after
+//     step 2 in program order);
+//  4. the last arrival, after its ticket came back and another compiler barrier, reads the partials
+//     with agent-scope (sc1) loads, which are served from the device-coherent level.
+// An acquire / release pair at agent scope would add an L2 write-back / invalidate of the XCD
+// (buffer_wbl2 / buffer_inv sc1): 52 us at the end of a forward that has just written GBs.
+__device__ __forceinline__ void publish_fence() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): this wave's stores are acknowledged
+  __asm__ __volatile__("" ::: "memory");           // and the compiler keeps every access on its side
+}
+
 template <bool DEC>
 __device__ __forceinline__ void finalize_stats_last(const KArgs& A, int ln) {
-  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0): this wave's partial stores are complete
+  publish_fence();
   unsigned int ticket = 0;
   if (ln == 0) ticket = __hip_atomic_fetch_add(A.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ticket = __builtin_amdgcn_readfirstlane(ticket);
   if (ticket != gridDim.x - 1) return;
+  __asm__ __volatile__("" ::: "memory");           // the partial loads stay behind the ticket
   const int ng = gridDim.x;
   double tot[5];
 #pragma unroll
@@ -3088,8 +3107,8 @@ __device__ void static_grad_chunk(const float* __restrict__ g0buf, const float* 
   __syncthreads();
   unsigned int* flag = reinterpret_cast<unsigned int*>(lds) + 3 * NOT * 256;   // behind the partial tiles
   if (w == 0) {
-    // device-coherent (sc1) stores, complete before the ticket (no agent-scope fence: see
-    // finalize_stats_last)
+    // device-coherent (sc1) stores, acknowledged before the ticket (publish_fence; the ordering
+    // argument and why no agent-scope fence: see finalize_stats_last)
     double* dst = reinterpret_cast<double*>(part + ((size_t)st * TCH + c) * NOT * 256);
 #pragma unroll
     for (int o = 0; o < NOT; ++o) {
@@ -3099,13 +3118,14 @@ __device__ void static_grad_chunk(const float* __restrict__ g0buf, const float* 
       __hip_atomic_store(dst + (o * 64 + lane) * 2 + 1, __builtin_bit_cast(double, __builtin_shufflevector(v, v, 2, 3)),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);
+    publish_fence();
     unsigned int ticket = 0;
     if (lane == 0) ticket = __hip_atomic_fetch_add(ctl + 1 + st, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) *flag = ticket;
   }
   __syncthreads();
   if (*flag != TCH - 1) return;                      // block-uniform
+  __asm__ __volatile__("" ::: "memory");             // the partial loads stay behind the ticket
   // last chunk of column tile st: the TCH partials in chunk order (device-coherent loads); element
   // (o, lane, e) is row o * 16 + 4 (lane / 16) + e, static column st * 16 + lane % 16
   const double* src = reinterpret_cast<const double*>(part + (size_t)st * TCH * NOT * 256);

@@ -323,7 +323,13 @@ class VAE:
             finally:
                 self._dp_w = None
             if "reducer" not in self._dp:
-                self._dp["reducer"] = udist.GradReducer(self.parameters(), average=False, group=self._dp["group"])
+                # one bucket group per stage, in registration order: autograd produces the decoder's
+                # gradients first, then the ODE's (the fused solve's tail hands them over at once),
+                # then the encoder's -- the decoder / ODE buckets are in flight while the encoder's
+                # backward still runs (a single 4 MB bucket would go out only after the last hook)
+                self._dp["reducer"] = udist.GradReducer(
+                    average=False, group=self._dp["group"],
+                    groups=[list(self.enc.parameters()), list(self.ode.parameters()), list(self.dec.parameters())])
             self._dp["reducer"].arm()
             loss.backward()
             # encoder + ODE + decoder gradients summed over the ranks, each bucket's all-reduce issued

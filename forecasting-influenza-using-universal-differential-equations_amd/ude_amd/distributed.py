@@ -210,38 +210,50 @@ def sync_side_stats(module, group=None) -> None:
 class GradReducer:
     """The data-parallel gradient all-reduce, overlapped with the rest of the backward (VERDICT r4
     item 6).  Parameters are split into buckets in reverse registration order (the order autograd
-    produces their gradients: the ODE's before the encoder's in the VAE, lib/VAE.py:200-223); a
-    post-accumulate-grad hook marks each parameter, and the moment a bucket's last parameter has its
-    gradient the bucket is flattened and its SUM all-reduce issued asynchronously -- on a side
-    stream for a HIP device (RCCL then runs while the backward's remaining kernels, e.g. the
-    encoder's, run on the compute stream), on gloo's worker thread on the CPU.  The fused solve
-    hands every ODE parameter's gradient over from its tail kernel at once, so the ODE bucket goes
-    out before autograd has even started on dy0's consumers.
+    produces their gradients: the decoder's, then the ODE's, then the encoder's in the VAE,
+    lib/VAE.py:200-223); ``groups`` (a list of parameter lists in registration order, e.g. one per
+    submodule) keeps every bucket inside one group, so a small model still gets one bucket per stage
+    instead of a single bucket completed only by the last hook.  A post-accumulate-grad hook marks
+    each parameter, and buckets are issued strictly in bucket-index order, as DDP does: bucket b goes
+    out the moment it and every bucket before it are complete, asynchronously -- on a side stream
+    for a HIP device (RCCL then runs while the backward's remaining kernels, e.g. the encoder's, run
+    on the compute stream), on gloo's worker thread on the CPU.  The issue order is therefore the
+    same on every rank whatever order the hooks fire in (a rank whose autograd reaches the buckets in
+    another order, or a parameter that got no gradient on one rank's shard, only delays the issue;
+    the collectives still pair up).  A bucket's flat buffer always covers every parameter of the
+    bucket (zeros for a parameter without a gradient on this rank), so its size is the same on every
+    rank; a parameter without a gradient gets the reduced slice unless that slice is all zero.
 
     ``arm()`` before the step's ``backward`` (the hooks do nothing otherwise, so other backward
-    passes -- pre-training, evaluation -- are untouched), ``finish()`` after it issues any bucket not yet issued (parameters that received no
-    gradient this step are left out, as in ``all_reduce_grads``), waits for the all-reduces, and
-    writes the summed (``average``: / world) gradients back.  Buckets are issued in the same order
-    on every rank because every rank runs the same graph.  ``log`` (when a list) receives
-    ("issue", bucket) / ("wait", bucket) in order: the CPU rehearsal's record of the overlap."""
+    passes -- pre-training, evaluation -- are untouched), ``finish()`` after it issues every bucket
+    not yet issued (in index order), waits for the all-reduces, and writes the summed (``average``:
+    / world) gradients back.  One backward per ``arm()``: a parameter whose hook fires twice in one
+    armed pass (gradient accumulation, a second loss, retain_graph) raises, since its bucket may
+    already be reduced.  ``log`` (when a list) receives ("grad", bucket) per hook, ("issue", bucket)
+    and ("wait", bucket) in order: the CPU rehearsal's record of the overlap."""
 
-    def __init__(self, params: Iterable[torch.nn.Parameter], average: bool = True, group=None,
-                 bucket_bytes: int = 4 << 20, log=None):
+    def __init__(self, params: Iterable[torch.nn.Parameter] = (), average: bool = True, group=None,
+                 bucket_bytes: int = 4 << 20, log=None, groups=None):
         self.group, self.average, self.log = group, average, log
-        ps = [p for p in params if p.requires_grad]
+        segs = [list(g) for g in groups] if groups is not None else [list(params)]
+        segs = [[p for p in g if p.requires_grad] for g in segs]
+        ps = [p for g in segs for p in g]
         self.buckets: List[List[torch.nn.Parameter]] = []
-        cur, size = [], 0
-        for p in reversed(ps):
-            cur.append(p)
-            size += p.numel() * p.element_size()
-            if size >= bucket_bytes:
+        for seg in reversed(segs):
+            cur, size = [], 0
+            for p in reversed(seg):
+                cur.append(p)
+                size += p.numel() * p.element_size()
+                if size >= bucket_bytes:
+                    self.buckets.append(cur)
+                    cur, size = [], 0
+            if cur:
                 self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
         self._where = {}
         for b, bucket in enumerate(self.buckets):
             for p in bucket:
+                if id(p) in self._where:
+                    raise ValueError("GradReducer: a parameter appears twice")
                 self._where[id(p)] = b
         self._hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in ps] if _active(group) else []
         self._stream = None
@@ -249,6 +261,8 @@ class GradReducer:
 
     def _reset(self):
         self._pending = [len(b) for b in self.buckets]
+        self._seen = set()
+        self._next = 0                      # the next bucket to issue (index order)
         self._inflight = {}                 # bucket -> (work, flat, params)
         self._armed = False
 
@@ -260,26 +274,39 @@ class GradReducer:
     def _ready(self, p):
         if not self._armed:
             return
+        if id(p) in self._seen:
+            raise RuntimeError("GradReducer: a parameter received a second gradient in one armed backward "
+                               "(one backward per arm(): accumulate with arm()/finish() around each backward, "
+                               "or reduce once after the last with all_reduce_grads)")
+        self._seen.add(id(p))
         b = self._where[id(p)]
         self._pending[b] -= 1
-        if self._pending[b] == 0 and b not in self._inflight:
-            self._issue(b)
+        if self.log is not None:
+            self.log.append(("grad", b))
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._issue(self._next)
+            self._next += 1
 
     def _issue(self, b):
-        ps = [p for p in self.buckets[b] if p.grad is not None]
-        if not ps:
-            self._inflight[b] = (None, None, ps)
-            return
-        dev = ps[0].grad.device
+        ps = self.buckets[b]
+        have = [p for p in ps if p.grad is not None]
+        if have:
+            dev, dt = have[0].grad.device, have[0].grad.dtype
+        else:
+            dev, dt = ps[0].device, ps[0].dtype
+
+        def flatten():
+            return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p, dtype=dt)).reshape(-1)
+                              for p in ps])
         if dev.type == "cuda":
             if self._stream is None:
                 self._stream = torch.cuda.Stream(dev)
             self._stream.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(self._stream):
-                flat = torch.cat([p.grad.reshape(-1) for p in ps])
+                flat = flatten()
                 work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
-            flat = torch.cat([p.grad.reshape(-1) for p in ps])
+            flat = flatten()
             work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight[b] = (work, flat, ps)
         if self.log is not None:
@@ -289,14 +316,12 @@ class GradReducer:
         if not _active(self.group):
             return
         assert self._armed, "GradReducer.finish() without arm() before the backward"
-        for b in range(len(self.buckets)):
-            if b not in self._inflight:
-                self._issue(b)
+        while self._next < len(self.buckets):
+            self._issue(self._next)
+            self._next += 1
         ws = dist.get_world_size(self.group)
         for b in range(len(self.buckets)):
             work, flat, ps = self._inflight[b]
-            if work is None:
-                continue
             work.wait()
             if self.log is not None:
                 self.log.append(("wait", b))
@@ -308,9 +333,13 @@ class GradReducer:
                 flat /= ws
             off = 0
             for p in ps:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                n = p.numel()
+                sl = flat[off:off + n].view_as(p)
                 off += n
+                if p.grad is not None:
+                    p.grad.copy_(sl)
+                elif bool(sl.ne(0).any()):
+                    p.grad = sl.clone()
         self._reset()
 
     def remove(self) -> None:

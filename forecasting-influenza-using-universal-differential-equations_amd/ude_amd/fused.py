@@ -9,6 +9,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
+import weakref
 
 import torch
 
@@ -33,8 +34,8 @@ class Plan:
     # control words of the *_ex calls, one zeroed buffer per stream (include/ude_rk4.h: zero on entry,
     # left zero by every call; calls sharing one are stream ordered)
     ctl: Dict[int, torch.Tensor] = field(default_factory=dict)
-    # packed weights of the last forward and the (storage, version) of every parameter they were
-    # packed from (``packed_weights``)
+    # packed weights of the last forward and (weak reference, storage, version) of every parameter
+    # they were packed from (``packed_weights``)
     pack_key: Optional[tuple] = None
     pack: Optional[torch.Tensor] = None
 
@@ -117,14 +118,17 @@ def _ctl(plan: Plan, dev) -> torch.Tensor:
     return c
 
 
-def _stats_out(dev):
-    """Fresh (mean (2), std (2), fa_norm (1)) outputs + fp64 totals (5) of one solve: separate tensors,
-    so posterior() and the tracker read them without a split (and their cotangents reach the kernel
-    without a concatenation); written by the forward kernel's last workgroup."""
-    mean = torch.empty(2, dtype=torch.float32, device=dev)
-    std = torch.empty(2, dtype=torch.float32, device=dev)
-    norm = torch.empty(1, dtype=torch.float32, device=dev)
-    sums = torch.empty(5, dtype=torch.float64, device=dev)
+def _stats_out(plan: Plan, dev):
+    """Fresh (mean (2), std (2), fa_norm (1)) outputs + fp64 totals (5) of one solve: separate views
+    of one buffer, so posterior() and the tracker read them without a split (and their cotangents
+    reach the kernel without a concatenation); written by the forward kernel's last workgroup.  The
+    kernel skips the statistics of a net the model lacks (mean / std of an Fa-only model, |Fa| of an
+    Fp-only one): those outputs are zero-filled, so no uninitialised value reaches autograd (their
+    zero cotangent terms, e.g. 2 g |Fa| in ``_StatSums``, stay zero)."""
+    kind = int(plan.desc.kind) & 3
+    buf = (torch.empty if kind == 3 else torch.zeros)(5, dtype=torch.float32, device=dev)
+    mean, std, norm = buf[0:2], buf[2:4], buf[4:5]
+    sums = (torch.empty if kind == 3 else torch.zeros)(5, dtype=torch.float64, device=dev)
     st = _native.UdeSideStats(mean.data_ptr(), std.data_ptr(), norm.data_ptr(), sums.data_ptr())
     return (mean, std, norm), sums, st
 
@@ -144,15 +148,28 @@ def _dstats(*grads):
     return _native.UdeSideStatsGrad(*[_ptr(g) for g in keep]), keep
 
 
+def _pack_key_matches(key, params) -> bool:
+    if key is None or len(key) != len(params):
+        return False
+    for (ref, ptr, ver), p in zip(key, params):
+        # the very tensor object (a weak reference: a freed module's parameters never match, even
+        # when the allocator hands a new module the same addresses and its version counters run
+        # through the same sequence), at the same storage, unmodified since the pack
+        if ref() is not p or ptr != p.data_ptr() or ver != p._version:
+            return False
+    return True
+
+
 def packed_weights(plan: Plan, params, dev) -> torch.Tensor:
-    """The fragment-order pack of a deterministic model's weights, re-packed only when a parameter's
-    storage or version counter changed since the last pack of this plan (an optimizer step, or any
+    """The fragment-order pack of a deterministic model's weights, re-packed only when the parameters
+    are not the very tensors of this plan's last pack (plans are shared by every module of the same
+    configuration), or one's storage or version counter changed since then (an optimizer step, or any
     in-place update through the parameter, bumps it).  Like autograd's own saved-tensor check, an
     in-place write through ``param.data`` is not seen by the version counter: call
     ``invalidate_packs()`` after such an edit."""
-    key = tuple((p.data_ptr(), p._version) for p in params)
-    if plan.pack is not None and plan.pack_key == key:
+    if plan.pack is not None and _pack_key_matches(plan.pack_key, params):
         return plan.pack
+    key = tuple((weakref.ref(p), p.data_ptr(), p._version) for p in params)
     ws = [p.contiguous() for p in params[0::2]]
     bs = [p.contiguous() for p in params[1::2]]
     pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
@@ -223,7 +240,7 @@ class FusedRK4(torch.autograd.Function):
         ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
             if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
-        stats, sums, st = _stats_out(dev)
+        stats, sums, st = _stats_out(plan, dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
         plan.lib.forward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),
@@ -358,7 +375,7 @@ def _dec_forward(plan: Plan, y0: torch.Tensor, pack: torch.Tensor, Wd: torch.Ten
     ckpt = torch.empty((sz.ckpt_bytes + sz.ckpt_final_bytes) // 4, dtype=torch.float32, device=dev)
     stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
     reg_slab = torch.empty(max(sz.grid_fwd, 1), dtype=torch.float64, device=dev)
-    stats, sums, st = _stats_out(dev)
+    stats, sums, st = _stats_out(plan, dev)
     reg = torch.empty(1, dtype=torch.float32, device=dev)
     if EVENTS is not None:
         e0 = _ev(dev); e0.record()
@@ -518,7 +535,7 @@ class FusedBayesRK4(torch.autograd.Function):
         ckpt = torch.empty(max(sz.ckpt_bytes // 4, 1), dtype=torch.float32, device=dev) \
             if (need_grad or keep_ckpt) else None
         stats_slab = torch.empty(max(sz.stats_slab_bytes // 8, 1), dtype=torch.float64, device=dev)
-        stats, sums, st = _stats_out(dev)
+        stats, sums, st = _stats_out(plan, dev)
         if EVENTS is not None:
             e0 = _ev(dev); e0.record()
         plan.lib.forward_ex(plan.desc, plan.prob, pack.data_ptr(), plan.sched_dev.data_ptr(), y0.data_ptr(),

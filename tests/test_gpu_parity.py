@@ -211,3 +211,37 @@ def test_cached_grid_follows_inplace_updates(pkg):
         with torch.no_grad():
             lat = pkg.odeint(mg, y0.to(DEV), td, method="rk4", options=dict(step_size=td[1] - td[0]))
         assert normwise_rel(lat, want) < 1e-5, scale
+
+
+def test_weight_pack_not_reused_across_modules(pkg):
+    """the weight pack is cached on the shared plan; a module freed and a new one of
+    the same configuration built in its place (same allocator addresses, the same parameter version
+    sequence: init + load_state_dict) must solve with ITS weights, not the freed module's pack."""
+    import gc
+    t = torch.arange(5, dtype=torch.float32)
+    gen = torch.Generator().manual_seed(3)
+    y0 = torch.cat([torch.rand(32, 1, 3, generator=gen) * 0.3 + 0.2, torch.randn(32, 1, 5, generator=gen)], -1).to(DEV)
+
+    def build(seed):
+        torch.manual_seed(seed)
+        m = pkg.FaFp(1, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+        m2 = pkg.FaFp(1, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+        m2.load_state_dict(m.state_dict())       # one version bump per parameter, like a checkpoint load
+        return m2.to(DEV)
+
+    def solve(m):
+        m.clear_tracking()
+        with torch.no_grad():
+            return pkg.odeint(m, y0, t, method="rk4", options=dict(step_size=1.0)).clone()
+
+    a = build(1)
+    lat_a = solve(a)
+    del a
+    gc.collect()
+    b = build(2)                                  # different weights, very likely a's addresses
+    lat_b = solve(b)
+    fresh = build(2)
+    pkg.ude_amd.fused.invalidate_packs()
+    lat_ref = solve(fresh)
+    assert not torch.equal(lat_a, lat_ref)
+    assert torch.equal(lat_b, lat_ref)

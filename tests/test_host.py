@@ -194,3 +194,24 @@ def test_development_build_at_product_path_is_refused(native, monkeypatch):
     with pytest.raises(native.UdeStaleLibrary):
         native.prebuilt()
     assert native._c_string('a "b" \\c') == 'a \\"b\\" \\\\c'
+
+
+def test_pack_key_requires_the_same_tensor_objects():
+    """the cached weight pack's key holds weak references to the very parameters it
+    was packed from: a parameter object that replaced a freed one at the same address and version
+    does not match, an in-place update (version bump) does not match, the same unmodified tensors do."""
+    import gc
+    import weakref
+    from ude_amd.fused import _pack_key_matches
+    ps = [torch.nn.Parameter(torch.randn(4, 3)), torch.nn.Parameter(torch.randn(4))]
+    key = tuple((weakref.ref(p), p.data_ptr(), p._version) for p in ps)
+    assert _pack_key_matches(key, ps)
+    with torch.no_grad():
+        ps[1].add_(1.0)
+    assert not _pack_key_matches(key, ps)
+    key = tuple((weakref.ref(p), p.data_ptr(), p._version) for p in ps)
+    ptrs = [p.data_ptr() for p in ps]
+    del ps
+    gc.collect()
+    qs = [torch.nn.Parameter(torch.randn(4, 3)), torch.nn.Parameter(torch.randn(4))]
+    assert not _pack_key_matches(key, qs), (ptrs, [q.data_ptr() for q in qs])

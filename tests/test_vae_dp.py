@@ -2,8 +2,8 @@
 
 ``VAE.train_step`` under a 2-rank process group (gloo) shards the batch's windows, makes the
 posterior / |Fa| statistics global before ``calc_loss``, weights every loss term by its share
-of the global loss and all-reduces the encoder + ODE + decoder gradients in one bucket before
-the grad-norm gate.  Checked against the single-process ``train_step`` on the same batch
+of the global loss and all-reduces the encoder + ODE + decoder gradients (one bucket per stage,
+issued in order during the backward) before the grad-norm gate.  Checked against the single-process ``train_step`` on the same batch
 (tests/golden/e2e_vae_us.npz inputs, eps replayed): global loss to 1e-6 relative, every
 gradient to 1e-5 normwise, identical parameters after the Adam step on both ranks.
 CPU: eager solver; GPU: both ranks on cuda:0 (the 1-GPU box) running the fused kernels."""
@@ -76,8 +76,17 @@ def _worker(rank, port, q, device):
         model = _model(g, device)
         assert model._dp is not None and model._dp["world"] == WORLD
         loss, grads, after = _step(model, g, device)
+        # the step's real reducer: one bucket group per stage, decoder / ODE / encoder in
+        # the order autograd produces them; a second step logs when each bucket went out
+        red = model._dp["reducer"]
+        red.log = []
+        _step(model, g, device)
+        buckets = [[id(p) for p in b] for b in red.buckets]
+        part = {id(p): name for name in ("enc", "ode", "dec") for p in getattr(model, name).parameters()}
+        layout = [sorted({part[i] for i in b}) for b in buckets]
         # numpy over the queue (torch tensors would be shared-memory handles of an exited process)
-        q.put((rank, loss, {k: v.numpy() for k, v in grads.items()}, {k: v.numpy() for k, v in after.items()}))
+        q.put((rank, loss, {k: v.numpy() for k, v in grads.items()}, {k: v.numpy() for k, v in after.items()},
+               layout, list(red.log)))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
@@ -98,8 +107,16 @@ def _run(device, port_off):
     assert all(r[0] != "err" for r in res), [r[1] for r in res if r[0] == "err"]
     g = load_golden("e2e_vae_us")
     ref_loss, ref_grads, ref_after = _step(_model(g, device), g, device)
+    for r in res:
+        layout, log = r[4], r[5]
+        assert layout == [["dec"], ["ode"], ["enc"]], layout
+        # the ODE bucket (1) is issued before the encoder's backward has produced any gradient, and
+        # every bucket goes out in index order
+        first_enc = min(i for i, e in enumerate(log) if e == ("grad", 2))
+        assert log.index(("issue", 1)) < first_enc, log
+        assert [e[1] for e in log if e[0] == "issue"] == [0, 1, 2], log
     res = [(r, l, {k: torch.from_numpy(v) for k, v in gr.items()}, {k: torch.from_numpy(v) for k, v in af.items()})
-           for r, l, gr, af in res]
+           for r, l, gr, af, _, _ in res]
     # the data-parallel step's gradients: against the single-process step 1e-5 (ODE parameters: the
     # fused solve's deterministic slabs, sums of the shards) and against the reference's fp64 step
     # under max(1e-4, 2 x the reference's own fp32 distance) (every parameter: the single-process e2e

@@ -477,15 +477,38 @@ def measure(pkg, udist, w, n_traj, dev, rank, world, steps, warmup, barrier):
     return el, kms, mod, len(t) - 1
 
 
-def extra_line(pkg, udist, name, dev, barrier, steps=3):
+def time_steps_graphed(pkg, udist, mod, y0, t, dlat, steps, warmup, dev):
+    """The same step replayed as a HIP graph (ude_amd/graphs.py GraphedStep: the pack, the fused
+    forward, the backward and its tail, the gradient accumulation -- one host call per step)."""
+    from ude_amd.graphs import GraphedStep
+    gs = GraphedStep(lambda: one_step(pkg, udist, mod, y0, t, dlat, 1), warmup=max(warmup, 1))
+    for _ in range(max(warmup, 1)):
+        gs.replay()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gs.replay()
+    _sync(dev)
+    return time.perf_counter() - t0
+
+
+def extra_line(pkg, udist, name, dev, barrier, steps=3, graphed=False):
+    """graphed: ms_per_step from HIP-graph replays of the step (the small-batch lines, host-bound when
+    eager); the eager step's time and its HIP-event kernel times are reported beside it."""
     w = WORKLOADS[name]
     m, y, t, d = build(pkg, w, dev, seed=7)
     el, k = time_steps(pkg, udist, m, y, t, d, 1, steps, 1, barrier, dev)
+    el_eager = el
+    if graphed:
+        el = time_steps_graphed(pkg, udist, m, y, t, d, steps, 3, dev)
     n_rk = len(t) - 1
     v = w["n_traj"] * n_rk * steps / el
     macs = macs_per_eval(w)
     out = {"workload": name, "description": w["desc"], "traj_steps_per_s": v, "rhs_evals_per_s": 4 * v,
            "ms_per_step": el / steps * 1e3, "fwd_ms": k["fwd"], "bwd_ms": k["bwd"]}
+    if graphed:
+        out["step_mode"] = "HIP graph replay (ude_amd.graphs.GraphedStep)"
+        out["ms_per_step_eager"] = el_eager / steps * 1e3
     if k["bwd"] and not w["kind"].startswith("Bayes_"):
         bwd_flop = 4 * 4 * macs * w["n_traj"] * n_rk
         fwd_flop = 4 * 2 * macs * w["n_traj"] * n_rk
@@ -609,9 +632,10 @@ def main():
         lines = [("north_star_M1", lambda: dict(extra_line(pkg, udist, "us_northstar", dev, barrier),
                                                 target_rhs_evals_per_s=1e7)),
                  ("north_star_M1_fp32", lambda: extra_line(pkg, udist, "us_fp32", dev, barrier)),
-                 ("M2_state49_n2048", lambda: extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=10)),
+                 ("M2_state49_n2048", lambda: extra_line(pkg, udist, "state49_n2048", dev, barrier, steps=20,
+                                                         graphed=True)),
                  ("state49_n2560_strong8_shard", lambda: extra_line(pkg, udist, "state49_n2560", dev, barrier,
-                                                                    steps=10)),
+                                                                    steps=20, graphed=True)),
                  ("M3_states_r1", lambda: extra_line(pkg, udist, "m3_states_r1", dev, barrier)),
                  ("bayes_M1", lambda: extra_line(pkg, udist, "bayes_us", dev, barrier)),
                  ("dopri5_state49", lambda: dopri5_line(pkg, w, dev)),

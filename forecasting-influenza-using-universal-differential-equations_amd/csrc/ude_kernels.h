@@ -1129,6 +1129,8 @@ struct RkAdjointEp {
       }
     }
     if (f0 >= M::F4) return;                       // padded feature rows
+    // DYF: the stage's flux part (parked by the flux pass) joins the MLP part first, one update
+    if constexpr (M::DYF) dY += *reinterpret_cast<const f4*>(rec + M::DYF_OFF + f0);
     f4* accy = reinterpret_cast<f4*>(rec + M::RK_ACCY + f0);
     f4* dk1 = reinterpret_cast<f4*>(rec + M::RK_DK1 + f0);
     f4* dk2 = reinterpret_cast<f4*>(rec + M::RK_DK2 + f0);
@@ -1582,7 +1584,7 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
     // the RK adjoint accumulators this stage updates, read with the other operands (every LDS
     // read of the item before its first write: one round trip)
     f4 ra[NQF], r1[NQF], r2[NQF], r3[NQF];
-    if constexpr (M::HAS_P) {
+    if constexpr (M::HAS_P && !M::DYF) {
 #pragma unroll
       for (int v = 0; v < NQF; ++v) {
         ra[v] = *reinterpret_cast<const f4*>(rec + M::RK_ACCY + f0 + 4 * v);
@@ -1686,6 +1688,11 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
       for (int v = 0; v < NQF; ++v) {
         const f4 dY = {dyf[4 * v], dyf[4 * v + 1], dyf[4 * v + 2], dyf[4 * v + 3]};
         const int f = f0 + 4 * v;
+        if constexpr (M::DYF) {
+          // parked for the stage's one adjoint update (RkAdjointEp, with the MLP part)
+          *reinterpret_cast<f4*>(rec + M::DYF_OFF + f) = dY;
+          continue;
+        }
         RkAdjointEp<M, SR>::rk_adjoint_update(dY, dt, jj, ra[v], r1[v], r2[v], r3[v],
                                               reinterpret_cast<f4*>(rec + M::RK_ACCY + f),
                                               reinterpret_cast<f4*>(rec + M::RK_DK1 + f),

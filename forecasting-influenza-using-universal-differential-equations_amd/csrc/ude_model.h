@@ -168,8 +168,16 @@ struct Model {
   static constexpr int RK_DK3 = RK_DK2 + F4;
   // FULL0 backward: per-trajectory static-feature input gradients summed over the solve
   static constexpr int DYS_OFF = RK_DK3 + F4;
+  // Small records (layer-0 input gradient split over the waves, SPLITX0; a rate net): the flux
+  // part of each stage-input gradient is parked in its own row (DYF) and joined with the MLP part
+  // before the ONE 3/8-rule adjoint update of the stage.  On trajectories whose infected share
+  // grows exponentially the two parts nearly cancel; added to the fp32 adjoint accumulators one
+  // after the other they cost ~20x the rounding of their sum (M1 Fp [32, 32]: dy0 5e-6 -> 3e-7
+  // from the exact VJP of the same forward; found by oracle/ude_korder.c, tests/test_kernel_order.py).
+  static constexpr bool DYF = HAS_P && (((F16 + (FULL0 ? S16 : 0)) / 16) < WAVES);
+  static constexpr int DYF_OFF = DYS_OFF + (FULL0 ? S16 : 0);
   static constexpr int REC_F = cmax(ACT_END, F16 + S16);
-  static constexpr int REC_B = DYS_OFF + (FULL0 ? S16 : 0);
+  static constexpr int REC_B = DYF_OFF + (DYF ? F4 : 0);
   // row stride == 4 (mod 64) floats: conflict-free b128 fragment reads, and rows
   // t and t+4 land 16 banks apart for the dW b32 reads.
   static constexpr int stride(int n) { return ((n + 59) / 64) * 64 + 4; }

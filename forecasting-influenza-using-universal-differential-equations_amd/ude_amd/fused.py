@@ -110,7 +110,15 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _ctl(plan: Plan, dev) -> torch.Tensor:
+    if _capturing():
+        # HIP-graph capture (ude_amd/graphs.py): the graph's own zeroed word (a memset node, re-zeroed
+        # every replay), not cached -- it lives in the graph's memory pool
+        return torch.zeros(max(int(plan.sizes.ctl_bytes) // 4, 1), dtype=torch.int32, device=dev)
     stream = _stream(dev)
     c = plan.ctl.get(stream)
     if c is None:
@@ -167,13 +175,18 @@ def packed_weights(plan: Plan, params, dev) -> torch.Tensor:
     in-place update through the parameter, bumps it).  Like autograd's own saved-tensor check, an
     in-place write through ``param.data`` is not seen by the version counter: call
     ``invalidate_packs()`` after such an edit."""
-    if plan.pack is not None and _pack_key_matches(plan.pack_key, params):
+    capturing = _capturing()
+    if not capturing and plan.pack is not None and _pack_key_matches(plan.pack_key, params):
         return plan.pack
     key = tuple((weakref.ref(p), p.data_ptr(), p._version) for p in params)
     ws = [p.contiguous() for p in params[0::2]]
     bs = [p.contiguous() for p in params[1::2]]
     pack = torch.empty(plan.sizes.pack_bytes // 4, dtype=torch.float32, device=dev)
     plan.lib.pack(plan.desc, [w.data_ptr() for w in ws], [b.data_ptr() for b in bs], pack.data_ptr(), _stream(dev))
+    if capturing:
+        # a captured step packs on every replay (the parameters may be updated in place between
+        # replays, e.g. by an optimizer step); the graph-pool pack is not cached
+        return pack
     plan.pack_key, plan.pack = key, pack
     return pack
 

@@ -89,3 +89,24 @@ class EvalMaskRecorder:
         self.masks = torch.stack(self._m)
         self.margin = torch.stack(self._g).amin(0)
         return self.masks
+
+
+def kernel_forward_store(pkg, mod, y0, t, step_size):
+    """The fused training forward (deterministic RHS, fp32, on mod's HIP device) with its training store
+    kept: (latent (T, N, R, L), every stage input the kernel evaluated (E, N, R, 3) fp32 -- read from the
+    store's checkpoints [tile][step][stage][3R][16] --, the solve's (mean, std, |Fa|) outputs), on the host."""
+    from ude_amd import fused, solvers
+    dev = next(mod.parameters()).device
+    yd = y0.to(dev).contiguous()
+    plan = solvers.plan_for(mod, yd, t, step_size)
+    mod.clear_tracking()
+    with torch.no_grad():
+        params = [p for lin in mod.ude_linears() for p in (lin.weight, lin.bias)]
+        lat, m, s, n, ckpt, _tok, _sums = fused.FusedRK4.apply(plan, yd, True, *params)
+    mod.clear_tracking()
+    N, R, _L = y0.shape
+    tiles = (N + 15) // 16
+    E = 4 * plan.prob.n_steps
+    dyn = ckpt[: tiles * E * 3 * R * 16].view(tiles, E, 3 * R, 16)
+    x = dyn.permute(1, 0, 3, 2).reshape(E, tiles * 16, R, 3)[:, :N]
+    return lat.cpu(), x.cpu().contiguous(), (m.cpu(), s.cpu(), n.cpu())

@@ -444,6 +444,22 @@ def read_pmc(name):
         return None
 
 
+def read_roofline_rocprof(name):
+    """The committed recomputation of the line's roofline from a rocprofv3 kernel trace of the same
+    command over the same timed calls (tools/roofline_trace.py), or None."""
+    p = os.path.join(REPO, "profiles", "roofline_rocprof_" + name + ".json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return {"file": os.path.relpath(p, REPO), "measured_at_commit": d["source"].get("commit"),
+                "rocprof_bwd_call_ms": d["rocprof_bwd_call_ms"], "rocprof_bwd_kernel_ms": d["rocprof_bwd_kernel_ms"],
+                "rocprof_frac": d["rocprof_frac"], "timed_calls": d["timed_calls"]}
+    except Exception:
+        return None
+
+
 def _launch_workers(n):
     """`bench.py --gpus N` run without a launcher: start N ranks under torch.distributed.run
     as a child process (before this process touches the GPU) and exit with its code."""
@@ -614,6 +630,8 @@ def main():
                          "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
                          "traffic": pmc, "traffic_source": PMC_SOURCE.get(args.workload + "_bwd"),
                          "avg_launch_ms": kms["bwd"],
+                         # the same span from a committed rocprofv3 trace of this command (timed calls only)
+                         "rocprof": read_roofline_rocprof(args.workload),
                          "algorithmic_flop_per_launch": bwd_flop_launch,
                          # the MFMA work the kernel issues (padded tiles, hoisted static features) per
                          # algorithmic MAC, and the MFMA pipe's busy fraction that implies

@@ -218,3 +218,51 @@ def test_controller_vector_passes_match_torch(pkg):
     lib.scaled_sumsq(n, ks[0].data_ptr(), y0.data_ptr(), y1.data_ptr(), 1e-8, 1e-6, ssq.data_ptr(), st)
     r = (ks[0] / (1e-8 + 1e-6 * torch.max(y0.abs(), y1.abs()))).double()
     assert abs(float(ssq[0]) / float((r * r).sum()) - 1) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_fused_adjoint_state49_slice_matches_oracle(pkg):
+    """odeint_adjoint on a 1,024-trajectory slice of the state49 batch (R = 49, the
+    bench's model with its output layers x 0.1 so no trajectory crosses the mask boundary, as
+    tests/test_full_size.py's whole-batch adjoint) against the fp64 oracle adjoint
+    (oracle/ude_oracle_adjoint.py: torchdiffeq's augmented backward restated) on the same slice -- the
+    same batch-shared step control, so the same step sequence up to rounding: latent <= 1e-5, dy0 and
+    every weight gradient <= max(1e-4, 2 x the fp32 oracle's own distance)."""
+    from torchdiffeq import odeint_adjoint
+    torch.manual_seed(0)
+    mod = pkg.FaFp(49, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64])
+    with torch.no_grad():
+        for seq in (mod.net, mod.aug_net):
+            seq[-1].weight.mul_(0.1)
+            seq[-1].bias.mul_(0.1)
+    y0 = _y0(1024, 49, torch.float32, seed=5)
+    t = torch.tensor([0.0, 1.0], dtype=torch.float32)
+    c = torch.randn((2,) + tuple(y0.shape), generator=torch.Generator().manual_seed(6))
+    rtol, atol = 1e-6, 1e-8
+    rhs = OracleRHS.from_module(mod, torch.float64).requires_grad_()
+    with torch.no_grad():
+        yr = odeint_dopri5(rhs, y0.double(), t, rtol=rtol, atol=atol)
+    dy0, dps = adjoint_backward(rhs, rhs.weights(), t, yr, c.double(), rtol, atol)
+    r32 = OracleRHS.from_module(mod, torch.float32).requires_grad_()
+    with torch.no_grad():
+        y32 = odeint_dopri5(r32, y0, t, rtol=rtol, atol=atol)
+    d32, p32 = adjoint_backward(r32, r32.weights(), t, y32, c, rtol, atol)
+    bar = lambda a, b: max(1e-4, 2.0 * normwise_rel(a, b))
+    mg = mod.to("cuda")
+    yg = y0.to("cuda").requires_grad_(True)
+    ys = odeint_adjoint(mg, yg, t.to("cuda"), rtol=rtol, atol=atol)
+    (ys * c.to("cuda")).sum().backward()
+    info = dict(mg.last_adjoint_info)
+    assert info["fused"], info
+    e_lat = normwise_rel(ys.detach(), yr)
+    e_dy0 = normwise_rel(yg.grad, dy0)
+    grads = [p.grad for lin in mg.ude_linears() for p in (lin.weight, lin.bias)]
+    e_p = [normwise_rel(a, b) for a, b in zip(grads, dps)]
+    print(f"adjoint state49 slice (1024 x R49, {info}): latent {e_lat:.1e}, dy0 {e_dy0:.1e} "
+          f"[fp32 oracle {normwise_rel(d32, dy0):.1e}], weights " +
+          ", ".join(f"{e:.1e} [{normwise_rel(p, b):.1e}]" for e, p, b in zip(e_p, p32, dps)))
+    assert e_lat < 1e-5
+    assert e_dy0 < bar(d32, dy0)
+    for i, (e, p, b) in enumerate(zip(e_p, p32, dps)):
+        assert e < bar(p, b), (i, e, bar(p, b))

@@ -181,7 +181,7 @@ def test_device_expm1f_equals_restatement_on_every_float():
 # ---------------------------------------------------------------------------------------------------
 # GPU: whole solves, forward bitwise, backward against the exact VJP of the same forward
 
-def _gpu_vjp(pkg, mod, y0, t, dl):
+def _gpu_vjp(pkg, mod, y0, t, dl, h=None):
     """fused forward + VJP with the posterior / |Fa| terms; the cotangents the kernel receives are the
     fp32 roundings of dl, DM, DS, DN (returned, for the oracle)."""
     mg = mod.to(DEV)
@@ -189,7 +189,7 @@ def _gpu_vjp(pkg, mod, y0, t, dl):
     yg = y0.to(DEV).requires_grad_(True)
     mg.clear_tracking()
     assert pkg.fusable(mg, yg)
-    lat = pkg.odeint(mg, yg, t, method="rk4", options=dict(step_size=t[1] - t[0]))
+    lat = pkg.odeint(mg, yg, t, method="rk4", options=dict(step_size=t[1] - t[0] if h is None else h))
     loss = (lat * dl.float().to(DEV)).sum()
     if mg.ode_type != "Fp":
         loss = loss + np.float32(DN) * torch.norm(torch.stack(mg.tracker))
@@ -205,11 +205,11 @@ def _gpu_vjp(pkg, mod, y0, t, dl):
     return lat.detach().cpu(), out
 
 
-def _check(pkg, mod, y0, t, dl, label):
-    h = t[1] - t[0]
+def _check(pkg, mod, y0, t, dl, label, h=None):
+    h = t[1] - t[0] if h is None else h
     mod = mod.to(DEV)
     lat_k, X_k, (m_k, s_k, n_k) = kernel_forward_store(pkg, mod, y0, t, h)
-    lat_v, got = _gpu_vjp(pkg, mod, y0, t, dl)
+    lat_v, got = _gpu_vjp(pkg, mod, y0, t, dl, h)
     assert torch.equal(lat_v, lat_k)                      # the same forward, bit for bit
     mod = mod.cpu()
     ko = KernelOrderOracle(OracleRHS.from_module(mod, torch.float32))
@@ -279,11 +279,9 @@ def _y0(N, R, L, seed):
 def test_kernel_equals_korder_on_golden_shapes(pkg, case):
     g = load_golden(case)
     mod = module_from_golden(pkg, g)
-    t, _h = step_of(g)
-    if g["meta"]["step"] != "t1-t0":
-        pytest.skip("the whole-solve check below uses step = t[1] - t[0]")
+    t, h = step_of(g)
     y0 = torch.from_numpy(g["y0"]).float()
-    _check(pkg, mod, y0, t, torch.from_numpy(g["dlatent"]), case)
+    _check(pkg, mod, y0, t, torch.from_numpy(g["dlatent"]), case, h)
 
 
 @pytest.mark.gpu

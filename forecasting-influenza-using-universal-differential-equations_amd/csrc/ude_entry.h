@@ -763,9 +763,8 @@ struct EvalOps {
     if (!done) {
       HIPCHK(hipFuncSetAttribute((const void*)&ude_eval_fwd_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_F));
       HIPCHK(hipFuncSetAttribute((const void*)&ude_eval_vjp_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize, M::LDS_B));
-      if (M::HOIST)
-        HIPCHK(hipFuncSetAttribute((const void*)&ude_dy0_static_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   TT * M::R * M::L * 4));
+      HIPCHK(hipFuncSetAttribute((const void*)&ude_bwd_tail_kernel<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 Tail<M>::LDS));
       done = true;
     }
     int cus = 0, of = 0, ob = 0;
@@ -778,6 +777,10 @@ struct EvalOps {
     return UDE_OK;
     }
   }
+  // workspace: dW slab [gb][SLAB_STRIDE], G0 + static partials (HOIST), the tail's ticket words
+  static int64_t ctl_off(int gb, int n_tiles) {
+    return ((int64_t)gb * M::SLAB_STRIDE + Ops<M>::static_ws_floats(n_tiles) + 3) & ~(int64_t)3;
+  }
   static int workspace(const UdeProblem* p, int device, int64_t* bytes) {
     if (M::BAYES) return UDE_E_UNSUPPORTED;      // each evaluation's sample is a deterministic RHS
     if (p->n_traj < 1) return UDE_E_INVALID;
@@ -785,7 +788,7 @@ struct EvalOps {
     int gf = 1, gb = 1;
     int rc = grids(device, n_tiles, &gf, &gb);
     if (rc) return rc;
-    *bytes = ((int64_t)gb * M::SLAB_STRIDE + Ops<M>::static_ws_floats(n_tiles)) * 4;
+    *bytes = (ctl_off(gb, n_tiles) + Ops<M>::CTL_WORDS) * 4;
     return UDE_OK;
   }
   static int forward(const UdeProblem* p, const float* pack, const float* x, float* f, float* rates, float* fa,
@@ -841,22 +844,15 @@ struct EvalOps {
     a.dx = dx; a.slab = slab; a.g0buf = g0buf;
     a.n_traj = p->n_traj; a.n_tiles = n_tiles; a.fa_w = p->fa_w;
     a.fout = fout; a.f_scale = f_scale;
+    unsigned int* ctl = reinterpret_cast<unsigned int*>(slab + ctl_off(gb, n_tiles));
+    a.ctl = ctl; a.n_ctl = (int)Ops<M>::CTL_WORDS;
     hipLaunchKernelGGL((ude_eval_vjp_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL((ude_grad_finalize_kernel<M>), dim3((M::SLAB_TOTAL + 63) / 64), dim3(256), 0, s,
-                       (const float*)slab, gb, dparams);
+    // gradient finalize, static-column dW and dx's static dims: one launch (no time sums here)
+    hipLaunchKernelGGL((ude_bwd_tail_kernel<M>), dim3(Tail<M>::blocks(n_tiles)), dim3(256), Tail<M>::LDS, s,
+                       (const float*)slab, gb, (const float*)g0buf, pack, x, (const float*)nullptr, p->n_traj,
+                       n_tiles, 0, part, ctl, dx, dparams);
     HIPCHK(hipGetLastError());
-    if (M::HOIST) {
-      hipLaunchKernelGGL((ude_static_partial_kernel<M>), dim3(M::STATIC_CHUNKS, M::STATIC_GROUPS), dim3(256), 0, s,
-                         (const float*)g0buf, x, p->n_traj, n_tiles, part);
-      HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((ude_static_reduce_kernel<M>), dim3((M::K0 * M::S + 255) / 256), dim3(256), 0, s,
-                         (const float*)part, dparams);
-      HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((ude_dy0_static_kernel<M>), dim3(n_tiles), dim3(256), TT * M::R * M::L * 4, s,
-                         (const float*)g0buf, pack, (const float*)nullptr, p->n_traj, 0, dx);
-      HIPCHK(hipGetLastError());
-    }
     return UDE_OK;
     }
   }

@@ -33,6 +33,8 @@ struct EArgs {
   float fa_w;
   float* fout;             // VJP (nullable): f_scale * f(x) (N, R, L) from the same launch
   float f_scale;
+  unsigned int* ctl;       // VJP (HOIST): the tail's ticket words, zeroed here for the launch behind
+  int n_ctl;
 };
 
 // f = RHS(x) of pair p from the record after mlp_forward (lib/models.py:130-150), scaled by `scale`
@@ -347,6 +349,8 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
 template <class M>
 __global__ __launch_bounds__(NTHREADS) void ude_eval_vjp_kernel(EArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  // the workspace's ticket words start at zero for ude_bwd_tail_kernel (same stream, next launch)
+  if (blockIdx.x == 0 && (int)threadIdx.x < a.n_ctl) a.ctl[threadIdx.x] = 0u;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w == 0) eval_vjp_body<M, 0>(a, lds);
   else if (w == 1) eval_vjp_body<M, 1>(a, lds);

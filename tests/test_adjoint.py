@@ -198,8 +198,9 @@ def test_fused_adjoint_matches_autograd_adjoint(pkg, norm):
 
 @pytest.mark.gpu
 def test_controller_vector_passes_match_torch(pkg):
-    """ude_lincomb (out = base + sum_j c_j k_j, one pass) and ude_scaled_sumsq (sum of squared error
-    ratios, fp32 tolerance, fp64 sums) against PyTorch on a ragged length."""
+    """ude_lincomb (out = base + sum_j c_j k_j, one pass; 16-byte and scalar kernels) and
+    ude_scaled_sumsq (sum of squared error ratios, fp32 tolerance, fp64 sums) against PyTorch on a
+    ragged length."""
     from ude_amd import _native, fused
     lib = _native.prebuilt()
     g = torch.Generator(device="cuda").manual_seed(6)
@@ -213,6 +214,13 @@ def test_controller_vector_passes_match_torch(pkg):
         lib.lincomb(n, base.data_ptr(), [k.data_ptr() for k in ks[:nk]], c.data_ptr(), out.data_ptr(), st)
         ref = base + sum(ks[j] * c[j] for j in range(nk))
         assert torch.allclose(out, ref, rtol=1e-6, atol=1e-6)
+        # pointers 4 bytes off 16-byte alignment take the scalar kernel: the same per-element
+        # operation order, so bitwise the 16-byte kernel's elements 1..n-1
+        out2 = torch.zeros(n, device="cuda")
+        lib.lincomb(n - 1, base.data_ptr() + 4, [k.data_ptr() + 4 for k in ks[:nk]], c.data_ptr(),
+                    out2.data_ptr() + 4, st)
+        torch.cuda.synchronize()
+        assert torch.equal(out2[1:], out[1:])
     ssq = torch.empty(_native.SUMSQ_WS, dtype=torch.float64, device="cuda")
     y0, y1 = ks[1], ks[2]
     lib.scaled_sumsq(n, ks[0].data_ptr(), y0.data_ptr(), y1.data_ptr(), 1e-8, 1e-6, ssq.data_ptr(), st)

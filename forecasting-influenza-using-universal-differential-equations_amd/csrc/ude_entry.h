@@ -770,7 +770,8 @@ struct EvalOps {
     int cus = 0, of = 0, ob = 0;
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&of, (const void*)&ude_eval_fwd_kernel<M>, NTHREADS, M::LDS_F));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_eval_vjp_kernel<M>, NTHREADS, M::LDS_B));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&ob, (const void*)&ude_eval_vjp_kernel<M>, eval_vjp_threads<M>(),
+                                                           M::LDS_B));
     const long mf = (long)cus * (of < 1 ? 1 : of), mb = (long)cus * (ob < 1 ? 1 : ob);
     *gf = (int)(n_tiles < mf ? n_tiles : mf);
     *gb = (int)(n_tiles < mb ? n_tiles : mb);
@@ -846,7 +847,7 @@ struct EvalOps {
     a.fout = fout; a.f_scale = f_scale;
     unsigned int* ctl = reinterpret_cast<unsigned int*>(slab + ctl_off(gb, n_tiles));
     a.ctl = ctl; a.n_ctl = (int)Ops<M>::CTL_WORDS;
-    hipLaunchKernelGGL((ude_eval_vjp_kernel<M>), dim3(gb), dim3(NTHREADS), M::LDS_B, s, a);
+    hipLaunchKernelGGL((ude_eval_vjp_kernel<M>), dim3(gb), dim3(eval_vjp_threads<M>()), M::LDS_B, s, a);
     HIPCHK(hipGetLastError());
     // gradient finalize, static-column dW and dx's static dims: one launch (no time sums here)
     hipLaunchKernelGGL((ude_bwd_tail_kernel<M>), dim3(Tail<M>::blocks(n_tiles)), dim3(256), Tail<M>::LDS, s,

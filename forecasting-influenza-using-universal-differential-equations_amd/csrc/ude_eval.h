@@ -221,18 +221,24 @@ __device__ __forceinline__ void eval_flux_backward(float* lds, const EArgs& A, i
   }
 }
 
-template <class M, int W>
+// SPLIT (eval_split<M>): waves 0-3 run this critical path without weight-gradient accumulators
+// (input gradients only, each phase's input-gradient fragments one phase ahead); waves 4-7
+// (eval_wbody) accumulate dW, the bias row sums and G0 from the same LDS operands on the same
+// barrier sequence -- the RK4 backward's SPLIT_BWD_L arrangement for one evaluation.
+template <class M, int W, bool SPLIT>
 __device__ void eval_vjp_body(const EArgs& A, float* lds) {
   constexpr int SR = M::SR_B;
   constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
   constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  constexpr bool PFX = SPLIT && M::PF_X && !WRegs<M, W, true, true>::ON;
   const int tid = threadIdx.x, lane = tid & 63;
   const int t16 = lane & 15, g = lane >> 4;
   float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
   const Rsrc rs = make_rsrc(A.pack, M::PACK_TOTAL * 4);
-  f4 dw[NDWn], dws[1], g0t[NZn], c1[NZn];
+  f4 dw[SPLIT ? 1 : NDWn], dws[1], g0t[NZn], c1[NZn];
+  f4 fxp[(PFX && M::WX_Q(W) > 0) ? M::WX_Q(W) : 1];
 #pragma unroll
-  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  for (int i = 0; i < (SPLIT ? 1 : NDWn); ++i) dw[i] = f4zero();
   WRegs<M, W, true, true> wr;                      // recomputes the forward: all fragments
   wr.load(rs, lane);
   #pragma unroll 1
@@ -264,6 +270,7 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
     for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
     __syncthreads();
     mlp_forward<M, W, SR>(rs, lds, c1, lane, wr);
+    if constexpr (PFX) load_x_frags<M, W, M::D - 1>(rs, lane, fxp + M::xq_base(W, M::D - 1));
     if (A.fout) eval_f_pairs<M, SR>(lds, A, n0, A.fout, A.f_scale);
     eval_flux_backward<M, SR>(lds, A, n0);
     // zero the padded rows of the final-layer gradient slots
@@ -284,7 +291,8 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
       }
     }
     __syncthreads();
-    mlp_backward<M, W, SR>(rs, rs, lds, dw, dws, g0t, lane, nullptr, EvalEp<M, SR>{lds + t16 * SR}, wr);
+    mlp_backward<M, W, SR, SPLIT, PFX>(rs, rs, lds, dw, dws, g0t, lane, nullptr, EvalEp<M, SR>{lds + t16 * SR}, wr,
+                                       nullptr, fxp);
     if constexpr (M::SPLITX0) {
       constexpr int NVX = cmin(M::F4, M::F16) / 4;
       #pragma unroll 1
@@ -309,53 +317,75 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
       }
     }
     // per-trajectory layer-0 output gradients -> G0 (static-feature gradients) + bias row sums
-    sfor<M::FT(0)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(0, k) == W) {
-        const f4 gv = g0t[M::nz_before(W, k)];
-        if constexpr (M::HOIST) {
-          float* dst = A.g0buf + ((size_t)tile * M::K0 + k * 16 + g * 4) * TT + t16;
-          dst[0] = gv[0]; dst[TT] = gv[1]; dst[2 * TT] = gv[2]; dst[3 * TT] = gv[3];
-        }
-        f4 r = gv;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) r[e] = row16_sum(r[e]);
-        if (t16 == 0) {
-          float* db = lds + M::DB_LDS + k * 16 + g * 4;
-          db[0] += r[0]; db[1] += r[1]; db[2] += r[2]; db[3] += r[3];
-        }
-      }
-    });
+    // (SPLIT: the partner waves')
+    if constexpr (!SPLIT) g0_tile_end<M, W>(A, lds, g0t, tile, lane);
     __syncthreads();
   }
 
-  sfor<M::D>([&](auto dd) {
-    constexpr int d = decltype(dd)::value;
-    sfor<M::FT(d)>([&](auto kk) {
-      constexpr int k = decltype(kk)::value;
-      if constexpr (M::fowner(d, k) == W) {
-        constexpr int net = M::fnet(d, k);
-        sfor<M::rti(net, d)>([&](auto cc) {
-          constexpr int ct = decltype(cc)::value;
-          reinterpret_cast<f4*>(myslab + (M::dyn_tiles_before(d, k) + ct) * 256)[lane] = dw[M::ndw_before(W, d, k) + ct];
-        });
-      }
-    });
-  });
+  if constexpr (SPLIT) lds_sync();                 // the partner waves' last bias row sums have landed
+  else dw_to_slab<M, W>(dw, dws, myslab, lane);
   #pragma unroll 1
   for (int i = tid; i < M::NDB; i += NTHREADS) myslab[M::SLAB_DB + i] = lds[M::DB_LDS + i];
 }
 
+// eval_vjp_body's partner wave W + 4 (SPLIT): one barrier for each of the critical path's, the weight
+// gradients of the backward phases (mlp_backward_dw_l, no data movement) and the tile's G0 rows.
+template <class M, int W>
+__device__ void eval_wbody(const EArgs& A, float* lds) {
+  constexpr int SR = M::SR_B;
+  constexpr int NDWn = M::NDW(W) > 0 ? M::NDW(W) : 1;
+  constexpr int NZn = M::NZ(W) > 0 ? M::NZ(W) : 1;
+  int lane = threadIdx.x & 63;
+  float* myslab = A.slab + (size_t)blockIdx.x * M::SLAB_STRIDE;
+  f4 dw[NDWn], g0t[NZn];
+#pragma unroll
+  for (int i = 0; i < NDWn; ++i) dw[i] = f4zero();
+  __builtin_amdgcn_s_setprio(1);                  // as bwd_wbody_l
+  lds_sync();                                     // record zeroed
+  for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
+    asm volatile("" : "+v"(lane));                // lane-derived addresses per tile (bwd_wbody_l)
+    lds_sync();                                   // evaluation point and cotangents in the record
+#pragma unroll
+    for (int i = 0; i < NZn; ++i) g0t[i] = f4zero();
+    lds_sync();                                   // static hoist
+    sfor<M::D>([&](auto) { lds_sync(); });        // the forward's layer phases
+    lds_sync();                                   // flux backward: final-layer gradients written
+    mlp_backward_dw_l<M, W, SR>(lds, dw, g0t, lane, [](auto) {});
+    lds_sync();                                   // layer-0 input-gradient epilogue
+    g0_tile_end<M, W>(A, lds, g0t, tile, lane);
+    lds_sync();                                   // dx written
+  }
+  f4 none[1];
+  dw_to_slab<M, W>(dw, none, myslab, lane);
+  lds_sync();                                     // bias row sums complete -> eval_vjp_body copies them
+}
+
+// the split evaluation + VJP where the RK4 backward is split the same way (large records)
 template <class M>
-__global__ __launch_bounds__(NTHREADS) void ude_eval_vjp_kernel(EArgs a) {
+constexpr bool eval_split() { return M::SPLIT_BWD_L; }
+template <class M>
+constexpr int eval_vjp_threads() { return eval_split<M>() ? 2 * NTHREADS : NTHREADS; }
+
+template <class M>
+__global__ __launch_bounds__(eval_vjp_threads<M>()) void ude_eval_vjp_kernel(EArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // the workspace's ticket words start at zero for ude_bwd_tail_kernel (same stream, next launch)
   if (blockIdx.x == 0 && (int)threadIdx.x < a.n_ctl) a.ctl[threadIdx.x] = 0u;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w == 0) eval_vjp_body<M, 0>(a, lds);
-  else if (w == 1) eval_vjp_body<M, 1>(a, lds);
-  else if (w == 2) eval_vjp_body<M, 2>(a, lds);
-  else eval_vjp_body<M, 3>(a, lds);
+  constexpr bool SPLIT = eval_split<M>();
+  if constexpr (SPLIT) {
+    if (w >= WAVES) {
+      if (w == 4) eval_wbody<M, 0>(a, lds);
+      else if (w == 5) eval_wbody<M, 1>(a, lds);
+      else if (w == 6) eval_wbody<M, 2>(a, lds);
+      else eval_wbody<M, 3>(a, lds);
+      return;
+    }
+  }
+  if (w == 0) eval_vjp_body<M, 0, SPLIT>(a, lds);
+  else if (w == 1) eval_vjp_body<M, 1, SPLIT>(a, lds);
+  else if (w == 2) eval_vjp_body<M, 2, SPLIT>(a, lds);
+  else eval_vjp_body<M, 3, SPLIT>(a, lds);
 }
 
 }  // namespace ude

@@ -1720,8 +1720,8 @@ __device__ __forceinline__ void flux_backward(float* lds, const KArgs& A, int n0
 // Tile end (deterministic RHS): per-trajectory layer-0 gradient sums -> global (the
 // static-feature gradients are computed from them by ude_static_*_kernel); their trajectory
 // sums -> the workgroup's bias row sums in LDS.
-template <class M, int W>
-__device__ __forceinline__ void g0_tile_end(const KArgs& A, float* lds, const f4* g0t, int tile, int lane) {
+template <class M, int W, class AT>
+__device__ __forceinline__ void g0_tile_end(const AT& A, float* lds, const f4* g0t, int tile, int lane) {
   const int t16 = lane & 15, g = lane >> 4;
   sfor<M::FT(0)>([&](auto kk) {
     constexpr int k = decltype(kk)::value;

@@ -41,10 +41,11 @@ struct EArgs {
 // (dims >= 3 zero, masked outside [-1, 2]).
 template <class M, int SR>
 __device__ __forceinline__ void eval_f_pairs(const float* lds, const EArgs& A, int n0, float* out, float scale) {
+  // row-mapped: consecutive lanes write consecutive (n, r) rows
+  const int nvalid = min(TT, A.n_traj - n0) * M::R;
   #pragma unroll 1
-  for (int p = threadIdx.x; p < M::PAIRS; p += NTHREADS) {
-    const int r = p / TT, t = p - r * TT, n = n0 + t;
-    if (n >= A.n_traj) continue;
+  for (int i = threadIdx.x; i < nvalid; i += NTHREADS) {
+    const int t = i / M::R, r = i - t * M::R;
     const float* rec = lds + t * SR;
     float Y[3], f[3];
 #pragma unroll
@@ -64,7 +65,7 @@ __device__ __forceinline__ void eval_f_pairs(const float* lds, const EArgs& A, i
         else f[c] = v;
       }
     }
-    float* dst = out + ((size_t)n * M::R + r) * M::L;
+    float* dst = out + ((size_t)n0 * M::R + i) * M::L;
 #pragma unroll
     for (int c = 0; c < 3; ++c) dst[c] = scale * ((Y[c] > 2.f || Y[c] < -1.f) ? 0.f : f[c]);
     for (int c = 3; c < M::L; ++c) dst[c] = 0.f;
@@ -221,6 +222,58 @@ __device__ __forceinline__ void eval_flux_backward(float* lds, const EArgs& A, i
   }
 }
 
+// Tile start of the evaluation + VJP: the evaluation point (dynamic dims -> Y slot, static dims ->
+// the static-feature columns) and the three cotangents -> record.  Row-mapped (consecutive lanes,
+// consecutive (n, r) rows of the tile's contiguous (16, R, L) block) with every load of the thread in
+// flight before the first LDS write: one HBM round trip per tile instead of one per row pass.
+template <class M, int SR>
+__device__ __forceinline__ void eval_tile_load(const EArgs& A, float* lds, int n0) {
+  constexpr int NROW = TT * M::R, PR = (NROW + NTHREADS - 1) / NTHREADS, LS = M::L - 3;
+  const int tid = threadIdx.x;
+  const int nvalid = min(TT, A.n_traj - n0) * M::R;
+  float xv[PR][M::L], cf[PR][3], cfa[PR][3], cr[PR][2];
+#pragma unroll
+  for (int u = 0; u < PR; ++u) {
+    const int i = tid + u * NTHREADS;
+    const bool ok = i < nvalid;
+    const size_t row = (size_t)n0 * M::R + (ok ? i : 0);
+#pragma unroll
+    for (int c = 0; c < M::L; ++c) xv[u][c] = ok ? A.x[row * M::L + c] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      cf[u][c] = ok ? A.cot_f[row * M::L + c] : 0.f;
+      cfa[u][c] = (ok && A.cot_fa) ? A.cot_fa[row * 3 + c] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) cr[u][c] = (ok && A.cot_rates) ? A.cot_rates[row * 2 + c] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PR; ++u) {
+    const int i = tid + u * NTHREADS;
+    if (i < NROW) {
+      const int t = i / M::R, r = i - t * M::R;
+      float* rec = lds + t * SR;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        rec[M::Y_OFF + 3 * r + c] = xv[u][c];
+        rec[M::RK_DK1 + 3 * r + c] = cf[u][c];
+        rec[M::RK_DK3 + 3 * r + c] = cfa[u][c];
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) rec[M::RK_DK2 + 2 * r + c] = cr[u][c];
+      if constexpr (M::S > 0) {
+#pragma unroll
+        for (int c = 0; c < LS; ++c) rec[M::XSB_OFF + LS * r + c] = xv[u][3 + c];
+      }
+    }
+  }
+  // the static columns' padding (the activation region aliases them in the recomputed forward)
+  if constexpr (M::S > 0 && M::S16 > M::S) {
+    constexpr int NP = M::S16 - M::S;
+    for (int i = tid; i < TT * NP; i += NTHREADS) lds[(i / NP) * SR + M::XSB_OFF + M::S + i % NP] = 0.f;
+  }
+}
+
 // SPLIT (eval_split<M>): waves 0-3 run this critical path without weight-gradient accumulators
 // (input gradients only, each phase's input-gradient fragments one phase ahead); waves 4-7
 // (eval_wbody) accumulate dW, the bias row sums and G0 from the same LDS operands on the same
@@ -247,23 +300,7 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
 
   for (int tile = blockIdx.x; tile < A.n_tiles; tile += gridDim.x) {
     const int n0 = tile * TT;
-    load_static<M, SR, M::XSB_OFF>(A.x, lds, n0, A.n_traj);
-    // evaluation point and the three cotangents -> record
-    #pragma unroll 1
-    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
-      const int r = p / TT, t = p - r * TT, n = n0 + t;
-      const bool valid = n < A.n_traj;
-      const size_t nr = valid ? (size_t)n * M::R + r : 0;
-      float* rec = lds + t * SR;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        rec[M::Y_OFF + 3 * r + c] = valid ? A.x[nr * M::L + c] : 0.f;
-        rec[M::RK_DK1 + 3 * r + c] = valid ? A.cot_f[nr * M::L + c] : 0.f;
-        rec[M::RK_DK3 + 3 * r + c] = (valid && A.cot_fa) ? A.cot_fa[nr * 3 + c] : 0.f;
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) rec[M::RK_DK2 + 2 * r + c] = (valid && A.cot_rates) ? A.cot_rates[nr * 2 + c] : 0.f;
-    }
+    eval_tile_load<M, SR>(A, lds, n0);
     __syncthreads();
     static_hoist<M, W, SR, M::XSB_OFF>(rs, lds, c1, lane);
 #pragma unroll
@@ -308,12 +345,13 @@ __device__ void eval_vjp_body(const EArgs& A, float* lds) {
     }
     __syncthreads();
     // dx (dynamic dims; static dims: ude_dy0_static_kernel from the G0 sums below)
-    #pragma unroll 1
-    for (int p = tid; p < M::PAIRS; p += NTHREADS) {
-      const int r = p / TT, t = p - r * TT, n = n0 + t;
-      if (n < A.n_traj) {
+    {
+      const int nvalid = min(TT, A.n_traj - n0) * M::R;    // row-mapped, as the tile start
+      #pragma unroll 1
+      for (int i = tid; i < nvalid; i += NTHREADS) {
+        const int t = i / M::R, r = i - t * M::R;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) A.dx[((size_t)n * M::R + r) * M::L + c] = lds[t * SR + M::RK_ACCY + 3 * r + c];
+        for (int c = 0; c < 3; ++c) A.dx[((size_t)n0 * M::R + i) * M::L + c] = lds[t * SR + M::RK_ACCY + 3 * r + c];
       }
     }
     // per-trajectory layer-0 output gradients -> G0 (static-feature gradients) + bias row sums

@@ -38,6 +38,7 @@ _C_MID = [6025192743 / 30085553152 / 2, 0.0, 51252292925 / 65400821598 / 2, -269
 MAX_NUM_STEPS = 2 ** 31 - 1
 
 
+
 # ---------------------------------------------------------------------------
 # fused (HIP) forward
 # ---------------------------------------------------------------------------
@@ -136,16 +137,18 @@ def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
     seg_t0 = t0
     last = None        # the last accepted step: (y, f(y), y1, f(y1), ks, dt)
     n_steps = 0
+    # one host read per attempt: the error ratio, the step's end time and the underflow / finiteness
+    # checks of its start travel together (the checks are raised in the same order, before the
+    # attempt is used); t_end_h mirrors the device t_end exactly (fp64 both)
+    tt_h = tt.tolist()
+    t_end_h = tt_h[0]
     for i in range(1, len(tt)):
         next_t = tt[i]
-        while next_t > t_end:
+        while tt_h[i] > t_end_h:
             if n_steps >= max_num_steps:
                 raise AssertionError("max_num_steps exceeded")
-            if not bool(t_end + dt > t_end):
-                raise AssertionError(f"underflow in dt {float(dt)}")
-            if not bool(torch.isfinite(y).all()):
-                raise AssertionError("non-finite values in state `y`")
             ts, te = t_end, t_end + dt
+            flags = torch.stack([torch.logical_not(te > ts), torch.logical_not(torch.isfinite(y).all())])
             dts = dt.to(ydt)
             ks = [fy]
             yi = y
@@ -160,10 +163,15 @@ def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
             else:
                 ratio = vec.ratio(err, y, y1)
             n_steps += 1
-            rf = float(ratio)                        # one host read per attempt
+            rf, te_h, underflow, nonfinite = torch.cat([ratio.detach().double().reshape(1), te.detach().reshape(1),
+                                                         flags.double()]).tolist()
+            if underflow:
+                raise AssertionError(f"underflow in dt {float(dt)}")
+            if nonfinite:
+                raise AssertionError("non-finite values in state `y`")
             if rf <= 1:
                 last = (y, fy, y1, f1, ks, dts)
-                seg_t0, t_end = ts, te
+                seg_t0, t_end, t_end_h = ts, te, te_h
                 y, fy = y1, f1
             if rf == 0:
                 dt = dt * 10.0

@@ -13,6 +13,10 @@ B="python3 $R/bench.py --no-extra --no-cpu-baseline"
 cd /tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks1 -o ks -- $B --steps 5 --warmup 2 > $O/ks1.log 2>&1 || exit 11
 find /tmp/ks1 -name "*kernel_stats.csv" -exec cp {} $O/state49_kernel_stats.csv \;
+# the roofline line recomputed from a kernel trace of the same command over its timed calls
+timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d /tmp/kt -o kt -- $B --steps 20 --warmup 5 > $O/bench_trace.json 2> $O/kt.log || exit 17
+find /tmp/kt -name "*kernel_trace.csv" -exec cp {} $O/state49_kernel_trace.csv \;
+python3 $R/tools/roofline_trace.py $O/state49_kernel_trace.csv $O/bench_trace.json ${UDE_COMMIT:-} > $O/roofline_rocprof_state49.json || exit 18
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks2 -o ks -- $B --workload us_northstar --steps 5 --warmup 2 > $O/ks2.log 2>&1 || exit 12
 find /tmp/ks2 -name "*kernel_stats.csv" -exec cp {} $O/m1_kernel_stats.csv \;
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ks3 -o ks -- $B --workload us_fp32 --steps 5 --warmup 2 > $O/ks3.log 2>&1 || exit 13

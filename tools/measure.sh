@@ -29,7 +29,7 @@ find /tmp/pf -name "*counter_collection.csv" -exec cp {} $O/pmc_fetch/ \;
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d /tmp/pw -o pw -- $B --steps 3 --warmup 1 > $O/pw.log 2>&1 || exit 15
 find /tmp/pw -name "*counter_collection.csv" -exec cp {} $O/pmc_write/ \;
 cd $R
-python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write state49 > $O/pmc_summary.txt 2>&1 || true
+UDE_ROOFLINE_JSON=$O/roofline_rocprof_state49.json python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write state49 > $O/pmc_summary.txt 2>&1 || true
 cp profiles/pmc_state49_*.json $O/ 2>/dev/null || true
 timeout -k 10 120 python -u tools/stage_profile.py state49 > $O/stage_state49.txt 2>&1 || exit 23
 timeout -k 10 120 python -u tools/stage_profile.py us_northstar > $O/stage_m1.txt 2>&1 || exit 24

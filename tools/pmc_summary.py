@@ -52,6 +52,15 @@ def main():
                "hbm_bytes_per_launch": (f_kib + w_kib) * 1024.0,
                "hbm_bytes_per_launch_if_fetch_x2": (2.0 * f_kib + w_kib) * 1024.0,
                "correction": "raw FETCH_SIZE + WRITE_SIZE (calibrated: dword-load reads count 1:1, see header)"}
+        # the kernel's average duration over the timed calls of the same commit (tools/roofline_trace.py
+        # output named by UDE_ROOFLINE_JSON), so the line's traffic and time come from one measured tree
+        rj = os.environ.get("UDE_ROOFLINE_JSON")
+        if rj and os.path.exists(rj):
+            t = json.load(open(rj))
+            key = {"bwd": "rocprof_bwd_kernel_ms", "fwd": "rocprof_fwd_ms"}.get(k)
+            if key in t:
+                rec["kernel_avg_ms"] = t[key]
+                rec["kernel_avg_ms_source"] = os.path.basename(rj) + " (kernel trace, timed calls)"
         with open(os.path.join(out_dir, f"pmc_{workload}_{k}.json"), "w") as f:
             json.dump(rec, f, indent=1)
         print(k, json.dumps(rec))

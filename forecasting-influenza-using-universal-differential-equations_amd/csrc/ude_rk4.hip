@@ -210,6 +210,19 @@ int ude_scaled_sumsq(int64_t n, const float* err, const float* y0, const float* 
   return ude::scaled_sumsq(n, err, y0, y1, atol, rtol, out, (hipStream_t)stream);
 }
 
+int ude_lincomb_hc(int64_t n, const float* base, const float* const* k, int32_t nk, const float* coef_host,
+                   float* out, ude_stream_t stream) {
+  if (!coef_host) return UDE_E_INVALID;
+  return ude::lincomb(n, base, k, nk, nullptr, out, (hipStream_t)stream, coef_host);
+}
+
+int ude_dopri_ratio(const float* err, const float* y0, const float* y1, double atol, double rtol, const double* ssq,
+                    const int64_t* n, int32_t n_pieces, const double* extra, int32_t n_extra, double dt,
+                    const unsigned char* flag, double* status, ude_stream_t stream) {
+  return ude::dopri_ratio(err, y0, y1, atol, rtol, ssq, n, n_pieces, extra, n_extra, dt, flag, status,
+                          (hipStream_t)stream);
+}
+
 int ude_pack_decoder(const UdeModelDesc* m, const float* W_dec, const float* b_dec, float* dec_pack,
                      ude_stream_t stream) {
   const Entry* e = find(m);

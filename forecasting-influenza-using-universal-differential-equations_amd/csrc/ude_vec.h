@@ -14,10 +14,11 @@ constexpr int LC_MAXK = 8;
 struct LcArgs {
   const float* base;            // nullable: 0
   const float* k[LC_MAXK];
-  const float* coef;            // device, nk floats
+  const float* coef;            // device, nk floats (null: the by-value copy cv)
   float* out;
   int64_t n;
   int nk;
+  float cv[LC_MAXK];            // coefficients passed by value (ude_lincomb_hc)
 };
 
 // out = base + sum_j coef[j] k_j; every term accumulated in the fixed order j = 0.. (k_0 first),
@@ -25,7 +26,7 @@ struct LcArgs {
 __global__ __launch_bounds__(256) void ude_lincomb_kernel(LcArgs a) {
   float c[LC_MAXK];
 #pragma unroll
-  for (int j = 0; j < LC_MAXK; ++j) c[j] = j < a.nk ? a.coef[j] : 0.f;
+  for (int j = 0; j < LC_MAXK; ++j) c[j] = j < a.nk ? (a.coef ? a.coef[j] : a.cv[j]) : 0.f;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
     float acc = a.k[0][i] * c[0];
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void ude_lincomb4_kernel(LcArgs a) {
   typedef float v4 __attribute__((ext_vector_type(4)));
   float c[LC_MAXK];
 #pragma unroll
-  for (int j = 0; j < LC_MAXK; ++j) c[j] = j < a.nk ? a.coef[j] : 0.f;
+  for (int j = 0; j < LC_MAXK; ++j) c[j] = j < a.nk ? (a.coef ? a.coef[j] : a.cv[j]) : 0.f;
   const int64_t n4 = a.n >> 2, stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
     v4 acc = reinterpret_cast<const v4*>(a.k[0])[i] * c[0];
@@ -91,12 +92,15 @@ __global__ __launch_bounds__(64) void ude_sumsq_finish_kernel(double* __restrict
   if (threadIdx.x == 0) out[0] = s;
 }
 
+// coef: device array (coef_host null) or host array copied into the launch (coef null)
 inline int lincomb(int64_t n, const float* base, const float* const* k, int nk, const float* coef, float* out,
-                   hipStream_t s) {
-  if (n < 0 || nk < 1 || nk > LC_MAXK || !k || !coef || !out) return -2;
+                   hipStream_t s, const float* coef_host = nullptr) {
+  if (n < 0 || nk < 1 || nk > LC_MAXK || !k || (!coef && !coef_host) || !out) return -2;
   if (n == 0) return 0;
   LcArgs a;
   a.base = base;
+  for (int j = 0; j < LC_MAXK; ++j) a.cv[j] = (coef_host && j < nk) ? coef_host[j] : 0.f;
+  if (coef_host) coef = nullptr;
   for (int j = 0; j < LC_MAXK; ++j) a.k[j] = j < nk ? k[j] : nullptr;
   for (int j = 0; j < nk; ++j)
     if (!k[j]) return -2;
@@ -113,6 +117,61 @@ inline int lincomb(int64_t n, const float* base, const float* const* k, int nk, 
   int64_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(ude_lincomb_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// One Dormand-Prince attempt's error ratio and next step size (torchdiffeq's mixed error norm and
+// _optimal_step_size, in PyTorch's own operation order so the controller's decisions match the operator
+// chain it replaces bit for bit: the fp32 tolerance of element 0, sqrt of each piece's fp64 sum times the
+// reciprocal of its count, NaN-propagating max, 0.9 * reciprocal(ratio^0.2) clamped to [dfac, 10]).
+struct RatioArgs {
+  const float* err;
+  const float* y0;
+  const float* y1;
+  const double* ssq;            // n_pieces sums at ssq + i * SSQ_STRIDE (ude_scaled_sumsq outputs)
+  const double* extra;          // nullable: n_extra more norm parts (fp64, device)
+  const unsigned char* flag;    // nullable: copied to status[2]
+  double* status;               // [ratio, next dt, flag]
+  double inv_n[4];
+  double dt;
+  float atol, rtol;
+  int n_pieces, n_extra;
+};
+constexpr int SSQ_STRIDE = SSQ_BLOCKS + 1;
+__device__ __forceinline__ double nanmax(double a, double b) { return (a != a || b != b) ? NAN : fmax(a, b); }
+__global__ void ude_dopri_ratio_kernel(RatioArgs a) {
+  if (threadIdx.x != 0) return;
+  const float u = fabsf(a.y0[0]), v = fabsf(a.y1[0]);
+  const float m = (u != u || v != v) ? NAN : fmaxf(u, v);
+  const float tol0 = __fadd_rn(a.atol, __fmul_rn(a.rtol, m));
+  double r = (double)fabsf(__fdiv_rn(a.err[0], tol0));
+  for (int i = 0; i < a.n_pieces; ++i) r = nanmax(r, sqrt(__dmul_rn(a.ssq[(size_t)i * SSQ_STRIDE], a.inv_n[i])));
+  for (int i = 0; i < a.n_extra; ++i) r = nanmax(r, a.extra[i]);
+  double dt;
+  if (r == 0.0) {
+    dt = __dmul_rn(a.dt, 10.0);
+  } else {
+    const double dfac = r < 1.0 ? 1.0 : 0.2;
+    double f = __dmul_rn(__ddiv_rn(1.0, pow(r, 0.2)), 0.9);
+    f = (f != f) ? f : fmin(fmax(f, dfac), 10.0);
+    dt = __dmul_rn(a.dt, f);
+  }
+  a.status[0] = r;
+  a.status[1] = dt;
+  a.status[2] = a.flag ? (double)a.flag[0] : 0.0;
+}
+
+inline int dopri_ratio(const float* err, const float* y0, const float* y1, double atol, double rtol, const double* ssq,
+                       const int64_t* n, int n_pieces, const double* extra, int n_extra, double dt,
+                       const unsigned char* flag, double* status, hipStream_t s) {
+  if (!err || !y0 || !y1 || !status || n_pieces < 0 || n_pieces > 4 || (n_pieces > 0 && (!ssq || !n)) ||
+      n_extra < 0 || (n_extra > 0 && !extra))
+    return -2;
+  RatioArgs a;
+  a.err = err; a.y0 = y0; a.y1 = y1; a.ssq = ssq; a.extra = extra; a.flag = flag; a.status = status;
+  for (int i = 0; i < 4; ++i) a.inv_n[i] = i < n_pieces ? 1.0 / (double)n[i] : 0.0;
+  a.dt = dt; a.atol = (float)atol; a.rtol = (float)rtol; a.n_pieces = n_pieces; a.n_extra = n_extra;
+  hipLaunchKernelGGL(ude_dopri_ratio_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

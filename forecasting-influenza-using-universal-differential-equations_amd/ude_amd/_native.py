@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = ("ude_supported", "ude_query", "ude_pack_weights", "ude_pack_
                     "ude_rhs_forward", "ude_rhs_vjp", "ude_pack_decoder", "ude_rk4_forward_dec",
                     "ude_decoder_backward", "ude_nll_workspace", "ude_nll_forward", "ude_nll_backward",
                     "ude_rhs_eval_vjp", "ude_lincomb", "ude_scaled_sumsq", "ude_build_info",
-                    "ude_rk4_forward_ex", "ude_rk4_forward_dec_ex", "ude_rk4_backward_ex")
+                    "ude_rk4_forward_ex", "ude_rk4_forward_dec_ex", "ude_rk4_backward_ex", "ude_lincomb_hc",
+                    "ude_dopri_ratio")
 SUMSQ_WS = 1025          # doubles of ude_scaled_sumsq's output / workspace (UDE_SUMSQ_WS)
 
 
@@ -175,6 +176,11 @@ class NativeLib:
         L.ude_lincomb.restype = i32
         L.ude_scaled_sumsq.argtypes = [ctypes.c_int64, vp, vp, vp, dbl, dbl, vp, vp]
         L.ude_scaled_sumsq.restype = i32
+        L.ude_lincomb_hc.argtypes = [ctypes.c_int64, vp, pvp, ctypes.c_int32, ctypes.POINTER(ctypes.c_float), vp, vp]
+        L.ude_lincomb_hc.restype = i32
+        L.ude_dopri_ratio.argtypes = [vp, vp, vp, dbl, dbl, vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, vp,
+                                      ctypes.c_int32, dbl, vp, vp, vp]
+        L.ude_dopri_ratio.restype = i32
         L.ude_build_info.argtypes = []
         L.ude_build_info.restype = ctypes.c_char_p
         pst, pdst = ctypes.POINTER(UdeSideStats), ctypes.POINTER(UdeSideStatsGrad)
@@ -297,6 +303,18 @@ class NativeLib:
     def lincomb(self, n, base, ks: Sequence[int], coef, out, stream) -> None:
         arr = (ctypes.c_void_p * len(ks))(*ks)
         check(self.lib.ude_lincomb(int(n), base, arr, len(ks), coef, out, stream), "ude_lincomb")
+
+    def lincomb_hc(self, n, base, ks: Sequence[int], coef: Sequence[float], out, stream) -> None:
+        """ude_lincomb with host coefficients (fp32 values, copied into the launch)."""
+        arr = (ctypes.c_void_p * len(ks))(*ks)
+        cv = (ctypes.c_float * len(coef))(*coef)
+        check(self.lib.ude_lincomb_hc(int(n), base, arr, len(ks), cv, out, stream), "ude_lincomb_hc")
+
+    def dopri_ratio(self, err, y0, y1, atol, rtol, ssq, ns: Sequence[int], extra, n_extra, dt, flag, status,
+                    stream) -> None:
+        na = (ctypes.c_int64 * max(len(ns), 1))(*ns)
+        check(self.lib.ude_dopri_ratio(err, y0, y1, float(atol), float(rtol), ssq, na, len(ns), extra, int(n_extra),
+                                       float(dt), flag, status, stream), "ude_dopri_ratio")
 
     def scaled_sumsq(self, n, err, y0, y1, atol, rtol, out, stream) -> None:
         check(self.lib.ude_scaled_sumsq(int(n), err, y0, y1, float(atol), float(rtol), out, stream),

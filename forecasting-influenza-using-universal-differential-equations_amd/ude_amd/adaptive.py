@@ -94,6 +94,96 @@ def _dot(ks: List[torch.Tensor], c: torch.Tensor) -> torch.Tensor:
     return acc
 
 
+def _initial_dt(func, y0, f0, t0, first_step, rt, at, _rms):
+    """torchdiffeq's ``_select_initial_step`` (fp64 device scalar), or the given first step."""
+    ydt, dev = y0.dtype, y0.device
+    if first_step is not None:
+        return torch.as_tensor(first_step, dtype=torch.float64, device=dev)
+    scale = at + torch.abs(y0) * rt
+    d0 = _rms(y0 / scale).abs()
+    d1 = _rms(f0 / scale).abs()
+    h0 = torch.tensor(1e-6, dtype=ydt, device=dev) if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    h0 = h0.abs()
+    f1 = func(t0.to(ydt) + h0, y0 + h0 * f0)
+    d2 = torch.abs(_rms((f1 - f0) / scale) / h0)
+    if d1 <= 1e-15 and d2 <= 1e-15:
+        h1 = torch.max(torch.tensor(1e-6, dtype=ydt, device=dev), h0 * 1e-3)
+    else:
+        h1 = (0.01 / torch.max(d1, d2)) ** (1.0 / 5.0)
+    return torch.min(100 * h0, h1.abs()).to(torch.float64)
+
+
+def host_scalar_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol, atol, first_step, max_num_steps: int, norm,
+                       hv) -> torch.Tensor:
+    """``eager_dopri5(..., vec=...)`` for an autonomous fused right-hand side (odeint_adjoint's fused
+    backward), with the controller's scalars on the host: the step size, step ends and stage
+    coefficients are mirrored exactly in Python (fp64 sums, fp32 coefficient products as PyTorch forms
+    them), the stage / error combinations take their coefficients by value (``hv.comb_hc``: ude_lincomb_hc)
+    and the error ratio and next step size come from one device kernel (``hv.ratio_dt``: ude_dopri_ratio)
+    read with the state's finiteness flag in ONE host transfer per attempt.  The same decisions and the
+    same arithmetic as the operator chain (tests/test_adjoint.py), without its ~60 scalar kernels per
+    attempt.  ``func(None, y)``: the evaluation time is not passed (the fused RHS ignores it)."""
+    import numpy as np
+    f32 = np.float32
+    ydt, dev = y0.dtype, y0.device
+    tt = t.to(device=dev, dtype=torch.float64)
+    tt_h = tt.tolist()
+    rt = torch.as_tensor(rtol, dtype=torch.float64, device=dev)
+    at = torch.as_tensor(atol, dtype=torch.float64, device=dev)
+    beta32 = [[f32(b) for b in row] for row in _BETA]
+    cerr32 = [f32(c) for c in _C_ERROR]
+    cmid32 = [f32(c) for c in _C_MID]
+    f0 = func(tt[0].to(ydt), y0)
+    dt_h = float(_initial_dt(func, y0, f0, tt[0], first_step, rt, at, norm))
+    out = [y0]
+    y, fy = y0, f0
+    t_end_h = seg_t0_h = tt_h[0]
+    last = None
+    n_steps = 0
+    nonfin = torch.logical_not(torch.isfinite(y).all())
+    for i in range(1, len(tt_h)):
+        while tt_h[i] > t_end_h:
+            if n_steps >= max_num_steps:
+                raise AssertionError("max_num_steps exceeded")
+            te_h = t_end_h + dt_h
+            if not te_h > t_end_h:
+                raise AssertionError(f"underflow in dt {dt_h}")
+            dts = f32(dt_h)
+            ks = [fy]
+            yi = y
+            for s in range(6):
+                yi = hv.comb_hc(y, ks, [b * dts for b in beta32[s]])
+                ks.append(func(None, yi))
+            y1, f1 = yi, ks[-1]
+            err = hv.comb_hc(None, ks, [c * dts for c in cerr32])
+            rf, dt_next, bad = hv.ratio_dt(err, y, y1, dt_h, nonfin)
+            if bad:
+                raise AssertionError("non-finite values in state `y`")
+            n_steps += 1
+            if rf <= 1:
+                last = (y, fy, y1, f1, ks, dts)
+                seg_t0_h, t_end_h = t_end_h, te_h
+                y, fy = y1, f1
+                nonfin = torch.logical_not(torch.isfinite(y).all())
+            dt_h = dt_next
+        yl, fyl, y1l, f1l, ksl, dts_l = last
+        # torchdiffeq's dense output with eager_dopri5's operations (0-dim fp32 device scalars)
+        dtl = torch.tensor(float(dts_l), dtype=ydt, device=dev)
+        y_mid = hv.comb_hc(yl, ksl, [c * dts_l for c in cmid32])
+        a = 2 * dtl * (f1l - fyl) - 8 * (y1l + yl) + 16 * y_mid
+        b = dtl * (5 * fyl - 3 * f1l) + 18 * yl + 14 * y1l - 32 * y_mid
+        c = dtl * (f1l - 4 * fyl) - 11 * yl - 5 * y1l + 16 * y_mid
+        coef = [yl, dtl * fyl, c, b, a]
+        x = torch.tensor(float(f32((tt_h[i] - seg_t0_h) / (t_end_h - seg_t0_h))), dtype=ydt, device=dev)
+        total = coef[0] + x * coef[1]
+        xp = x
+        for cc in coef[2:]:
+            xp = xp * x
+            total = total + xp * cc
+        out.append(total)
+    return torch.stack(out, 0)
+
+
 def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, first_step=None,
                  max_num_steps: int = MAX_NUM_STEPS, norm=None, vec=None) -> torch.Tensor:
     """``norm``: torchdiffeq's error norm (default the RMS over every element, ``_rms_norm``);
@@ -115,21 +205,7 @@ def eager_dopri5(func, y0: torch.Tensor, t: torch.Tensor, rtol=1e-7, atol=1e-9, 
 
     t0 = tt[0]
     f0 = func(t0.to(ydt), y0)
-    if first_step is None:
-        scale = at + torch.abs(y0) * rt
-        d0 = _rms(y0 / scale).abs()
-        d1 = _rms(f0 / scale).abs()
-        h0 = torch.tensor(1e-6, dtype=ydt, device=dev) if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
-        h0 = h0.abs()
-        f1 = func(t0.to(ydt) + h0, y0 + h0 * f0)
-        d2 = torch.abs(_rms((f1 - f0) / scale) / h0)
-        if d1 <= 1e-15 and d2 <= 1e-15:
-            h1 = torch.max(torch.tensor(1e-6, dtype=ydt, device=dev), h0 * 1e-3)
-        else:
-            h1 = (0.01 / torch.max(d1, d2)) ** (1.0 / 5.0)
-        dt = torch.min(100 * h0, h1.abs()).to(torch.float64)
-    else:
-        dt = torch.as_tensor(first_step, dtype=torch.float64, device=dev)
+    dt = _initial_dt(func, y0, f0, t0, first_step, rt, at, _rms)
 
     out = [y0]
     y, fy = y0, f0

@@ -23,7 +23,9 @@ ude_amd.adaptive.eager_dopri5 or the fixed grids.  For a deterministic UDE modul
 (``_FusedAug``): the weights are packed once, every reversed augmented evaluation
 ``(-vjp_t, -f, a^T df/dy, a^T df/dtheta)`` is ONE gfx950 launch (ude_rhs_eval_vjp: evaluation and
 VJP, written straight into the flat derivative), and the Dormand-Prince stage / error / dense-output
-combinations are single passes (ude_lincomb, ude_scaled_sumsq).  Otherwise every augmented
+combinations are single passes (ude_lincomb_hc, ude_scaled_sumsq) and the controller's scalars live on
+the host (``adaptive.host_scalar_dopri5``: one read of the device error ratio / next step size per
+attempt, ude_dopri_ratio).  Otherwise every augmented
 evaluation calls the RHS module and ``torch.autograd.grad`` through it (for the UDE modules on a
 HIP device one evaluation kernel + one VJP kernel, ude_amd/eval_rhs.py).
 """
@@ -98,6 +100,7 @@ class _FusedAug:
         self.psizes = [int(p.numel()) for p in adjoint_params]
         self.seminorm = seminorm
         self.ssq = torch.empty(2 * SUMSQ_WS, dtype=torch.float64, device=y.device)
+        self.status = torch.zeros(3, dtype=torch.float64, device=y.device)
         self.evals = 0
 
     @staticmethod
@@ -130,6 +133,33 @@ class _FusedAug:
         self._keep = c                                    # alive until the stream has read it
         return out
 
+    def comb_hc(self, base, ks, coef) -> torch.Tensor:
+        """base + sum_j coef[j] ks[j] with host (fp32) coefficients: ude_lincomb_hc."""
+        out = torch.empty_like(ks[0])
+        self.lib.lincomb_hc(out.numel(), None if base is None else base.data_ptr(), [k.data_ptr() for k in ks],
+                            [float(c) for c in coef], out.data_ptr(), self.stream)
+        return out
+
+    def ratio_dt(self, err, y, y1, dt: float, nonfinite: torch.Tensor):
+        """(error ratio, next step size, non-finite flag) of one attempt in one host read: the y / a_y
+        pieces' sums of squares (ude_scaled_sumsq), the parameter pieces' RMS as ratio() forms them
+        (mixed norm only), then ude_dopri_ratio."""
+        n = self.nrl
+        for i, off in enumerate((1, 1 + n)):
+            self.lib.scaled_sumsq(n, err.data_ptr() + 4 * off, y.data_ptr() + 4 * off, y1.data_ptr() + 4 * off,
+                                  self.atol, self.rtol, self.ssq.data_ptr() + 8 * i * SUMSQ_WS, self.stream)
+        extra, n_extra = None, 0
+        if not self.seminorm and self.psizes:
+            off = 1 + 2 * n
+            r = err[off:] / (self.atol + self.rtol * torch.max(y[off:].abs(), y1[off:].abs()))
+            extra = torch.stack([_rms(x).double() for x in torch.split(r, self.psizes)])
+            n_extra = extra.numel()
+        self.lib.dopri_ratio(err.data_ptr(), y.data_ptr(), y1.data_ptr(), self.atol, self.rtol, self.ssq.data_ptr(),
+                             [n, n], None if extra is None else extra.data_ptr(), n_extra, dt, nonfinite.data_ptr(),
+                             self.status.data_ptr(), self.stream)
+        rf, dt_next, bad = self.status.tolist()
+        return rf, dt_next, bad != 0.0
+
     def ratio(self, err, y, y1, atol: float, rtol: float) -> torch.Tensor:
         n = self.nrl
         for i, off in enumerate((1, 1 + n)):
@@ -160,17 +190,16 @@ def _solve_segment(aug_func, flat: _Flat, state: List[torch.Tensor], t_from, t_t
         return out
 
     opts = dict(options or {})
-    if method == "dopri5":
-        norm = lambda v: norm_of_tuple(flat.split(v))
-        vec = None
-        if fused is not None:
-            class _Vec:
-                comb = staticmethod(fused.comb)
-                ratio = staticmethod(lambda err, y, y1: fused.ratio(err, y, y1, float(atol), float(rtol)))
-            vec = _Vec
-        sol = _adaptive.eager_dopri5(f_rev if fused is None else fused, y0, s_pair, rtol, atol,
-                                     opts.pop("first_step", None), opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS),
-                                     norm=norm, vec=vec)
+    if method == "dopri5" and fused is not None:
+        # the fused backward: host-mirrored controller scalars, one host read per attempt
+        fused.atol, fused.rtol = float(atol), float(rtol)
+        sol = _adaptive.host_scalar_dopri5(fused, y0, s_pair, rtol, atol, opts.pop("first_step", None),
+                                           opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS),
+                                           lambda v: norm_of_tuple(flat.split(v)), fused)
+    elif method == "dopri5":
+        sol = _adaptive.eager_dopri5(f_rev, y0, s_pair, rtol, atol, opts.pop("first_step", None),
+                                     opts.pop("max_num_steps", _adaptive.MAX_NUM_STEPS),
+                                     norm=lambda v: norm_of_tuple(flat.split(v)))
     elif method in ("rk4", "euler", "midpoint"):
         from .solvers import eager_fixed_grid
         sol = eager_fixed_grid(f_rev if fused is None else fused, y0, s_pair, method, opts.pop("step_size", None))

@@ -342,6 +342,20 @@ int ude_lincomb(int64_t n, const float* base, const float* const* k, int32_t nk,
                 ude_stream_t stream);
 int ude_scaled_sumsq(int64_t n, const float* err, const float* y0, const float* y1, double atol, double rtol,
                      double* out, ude_stream_t stream);
+/* ude_lincomb_hc: ude_lincomb with the nk coefficients in a HOST array, copied into the launch (the
+ * controller forms them from its exact host mirror of dt: no device scalar arithmetic per stage).
+ * ude_dopri_ratio: one attempt's error ratio and next step size on the device, status[0..2] (device fp64)
+ * = [ratio, next dt, *flag (nullable: 0)]: ratio = max(|err[0] / (atol + rtol max(|y0[0]|, |y1[0]|))| (fp32
+ * tolerance), sqrt(ssq[i * UDE_SUMSQ_WS] / n[i]) for the n_pieces <= 4 sums of ude_scaled_sumsq, extra[0 ..
+ * n_extra)) (NaN-propagating), next dt = dt * 10 at ratio 0, else dt * clamp(0.9 / ratio^0.2, ratio < 1 ? 1 :
+ * 0.2, 10) -- torchdiffeq's mixed norm and _optimal_step_size (torchdiffeq/_impl/rk_common.py), in
+ * PyTorch's operation order; one host read per attempt.  Replace the per-attempt operator chains of the
+ * adaptive controller (odeint_adjoint's fused backward). */
+int ude_lincomb_hc(int64_t n, const float* base, const float* const* k, int32_t nk, const float* coef_host,
+                   float* out, ude_stream_t stream);
+int ude_dopri_ratio(const float* err, const float* y0, const float* y1, double atol, double rtol, const double* ssq,
+                    const int64_t* n, int32_t n_pieces, const double* extra, int32_t n_extra, double dt,
+                    const unsigned char* flag, double* status, ude_stream_t stream);
 
 /* Library build tag (for logs / tests). */
 const char* ude_build_info(void);

@@ -229,6 +229,46 @@ def test_controller_vector_passes_match_torch(pkg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seminorm", [False, True])
+def test_host_scalar_controller_equals_operator_chain(pkg, seminorm):
+    """adaptive.host_scalar_dopri5 (odeint_adjoint's fused backward: controller scalars mirrored on the
+    host, ude_lincomb_hc / ude_dopri_ratio) against eager_dopri5 with the fused evaluation and the
+    device-scalar operator chain (ude_lincomb with device coefficients, PyTorch ratio and step-size
+    update): the same attempts and bitwise the same solution, mixed norm and seminorm."""
+    from ude_amd import adaptive
+    from ude_amd import adjoint as A
+    torch.manual_seed(7)
+    mod = pkg.FaFp(49, latent_dim=8, net_sizes=[64, 64, 32], aug_net_sizes=[64, 64]).to("cuda")
+    y = _y0(300, 49, torch.float32).to("cuda")
+    a = torch.randn(y.shape, generator=torch.Generator().manual_seed(8)).to("cuda")
+    params = tuple(p for lin in mod.ude_linears() for p in (lin.weight, lin.bias))
+    rtol, atol = 1e-6, 1e-8
+    fused = A._FusedAug(mod, y, params, seminorm)
+    fused.atol, fused.rtol = atol, rtol
+    zero = torch.zeros((), device="cuda")
+    state = [zero, y, a] + [torch.zeros_like(p) for p in params]
+    flat = A._Flat([x.shape for x in state])
+    y0 = flat.flat(state)
+    s_pair = torch.tensor([-1.5, -0.7], dtype=torch.float64, device="cuda")
+
+    def norm(v):
+        vt, yy, ay, *ap = flat.split(v)
+        n = torch.max(torch.stack([vt.abs().reshape(()), A._rms(yy), A._rms(ay)]))
+        return n if seminorm else torch.max(n, A._mixed_norm(ap))
+
+    class Vec:
+        comb = staticmethod(fused.comb)
+        ratio = staticmethod(lambda err, yy, y1: fused.ratio(err, yy, y1, atol, rtol))
+    e0 = fused.evals
+    r_old = adaptive.eager_dopri5(fused, y0, s_pair, rtol, atol, None, adaptive.MAX_NUM_STEPS, norm=norm, vec=Vec)
+    e1 = fused.evals
+    r_new = adaptive.host_scalar_dopri5(fused, y0, s_pair, rtol, atol, None, adaptive.MAX_NUM_STEPS, norm, fused)
+    e2 = fused.evals
+    assert e2 - e1 == e1 - e0 and e1 - e0 > 20
+    assert torch.equal(r_new, r_old), float((r_new - r_old).abs().max())
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_fused_adjoint_state49_slice_matches_oracle(pkg):
     """odeint_adjoint on a 1,024-trajectory slice of the state49 batch (R = 49, the

@@ -17,6 +17,7 @@ CASES = [  # kind, R, L, net, aug
     ("FaFp", 1, 8, [64, 64, 32], [64, 64]), ("Fp", 1, 8, [32, 32], None), ("Fa", 1, 8, None, [64, 64]),
     ("FaFp", 3, 5, [40, 24], [36]), ("FaFp", 10, 8, [64, 64, 32], [64, 64]), ("FaFp", 49, 8, [64, 64, 32], [64, 64]),
     ("Fp", 49, 8, [64, 64, 32], None), ("Fa", 10, 8, None, [64, 64]),
+    ("Fa", 49, 8, None, [64, 64]),     # the three R = 49 kinds run the split (8-wave) evaluation + VJP
 ]
 
 

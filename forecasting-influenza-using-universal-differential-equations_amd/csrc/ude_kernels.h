@@ -311,6 +311,13 @@ __device__ __forceinline__ void load_x_frags(Rsrc rs, int lane, f4* fx) {
   });
 }
 
+// Layer 0 of a record with at most 4 dynamic features (R = 1: S, I, R) and the static ones hoisted: every
+// K step but the first multiplies padding, so the phase runs ONE MFMA per output tile with lane (o, g)
+// holding W[o][g] and feature g instead of KP / 4 -- the same non-zero products added in the same order
+// (the padded steps add exact zeros), so bitwise the same layer output.
+template <class M>
+constexpr bool pack0() { return M::HOIST && M::F <= 4 && M::F16 == 16; }
+
 // Register-resident weights (Model::WREG): every fragment / bias quad wave W reads in the
 // forward (and, BWD, the input-gradient fragments), loaded once per launch.
 struct NoWRegs {
@@ -323,7 +330,9 @@ struct WRegs {
   static constexpr bool NEED_F = NEED_F_;   // a stored-activation RK4 backward never runs the forward
   static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
   static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
+  static constexpr int NP0 = (ON && NEED_F && pack0<M>()) ? M::NZ(W) : 0;
   f4 wf[NF > 0 ? NF : 1], wb[NB > 0 ? NB : 1], wx[NX > 0 ? NX : 1];
+  float w0[NP0 > 0 ? NP0 : 1];              // pack0: lane (o, g)'s layer-0 weight W[o][g]
   __device__ __forceinline__ void load(Rsrc rs, int lane, bool wait = true) {
     if constexpr (ON) {
       const int g = lane >> 4;
@@ -345,6 +354,19 @@ struct WRegs {
       // "pending" at the step loop's head and puts a vmcnt(0) before the first MFMA of every
       // stage, which also drains the loads prefetched a stage ahead (s_waitcnt vmcnt(0))
       if (wait) __builtin_amdgcn_s_waitcnt(0x0F70);
+      if constexpr (NP0 > 0) {
+        // lane (o, g) takes element g of lane (o, 0)'s fragment quad (W[o][0..3]), once per launch
+        sfor<M::FT(0)>([&](auto kk) {
+          constexpr int k = decltype(kk)::value;
+          if constexpr (M::fowner(0, k) == W) {
+            const f4 q = wf[M::fq_base(W, 0) + M::fq_before(W, 0, k)];
+            const int src = lane & 15;
+            const float v0 = __shfl(q[0], src, 64), v1 = __shfl(q[1], src, 64);
+            const float v2 = __shfl(q[2], src, 64), v3 = __shfl(q[3], src, 64);
+            w0[M::nz_before(W, k)] = g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+          }
+        });
+      }
     }
   }
 };
@@ -372,13 +394,22 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     // before its first MFMA -- unless they would not fit next to the working set (the Bayesian
     // state model's layer 0, K = 416: 208 VGPRs, spilled at the forward's 256): then chunk by chunk
     constexpr bool CHUNK_A = !RW && NF > 24;
+    constexpr bool P0 = d == 0 && pack0<M>();
     f4 fr[(NF > 0 && !RW && !CHUNK_A) ? NF : 1], bias[(M::FT(d) > 0 && !RW) ? M::FT(d) : 1];
+    float w0s[(P0 && !RW && M::NZ(W) > 0) ? M::NZ(W) : 1];
     if constexpr (!RW) {
       sfor<M::FT(d)>([&](auto kk) {
         constexpr int k = decltype(kk)::value;
         if constexpr (M::fowner(d, k) == W) {
           constexpr int net = M::fnet(d, k), rt = M::frt(d, k), KP = M::kin(net, d);
-          if constexpr (!CHUNK_A) load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
+          if constexpr (P0) {
+            // W[o][g]: element g of lane (o, 0)'s fragment quad
+            w0s[M::nz_before(W, k)] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((lane & 15) * 4 + g) * 4,
+                                                            (M::wf_off(net, d) + rt * (KP / 16) * 256) * 4, 0));
+          } else if constexpr (!CHUNK_A) {
+            load_frags<KP, M::wf_off(net, d) + rt * (KP / 16) * 256>(rs, lane, fr + M::fq_before(W, d, k));
+          }
           if constexpr (M::has_bias(d)) bias[k] = ldw(rs, g * 16, (M::b_off(net, d) + rt * 16) * 4);
         }
       });
@@ -398,9 +429,22 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
         else acc[k] = bias[k];
       }
     });
+    if constexpr (P0) {
+      // pack0: one MFMA per owned tile, lane (t, g) supplies feature g of trajectory t
+      const float xg = g < M::F ? rec[M::Y_OFF + g] : 0.f;
+      sfor<M::FT(d)>([&](auto kk) {
+        constexpr int k = decltype(kk)::value;
+        if constexpr (M::fowner(d, k) == W) {
+          float wv;
+          if constexpr (RW) wv = wr.w0[M::nz_before(W, k)];
+          else wv = w0s[M::nz_before(W, k)];
+          acc[k] = mfma4(wv, xg, acc[k]);
+        }
+      });
+    }
     // the wave's tiles of one net share the B operand (the layer input): one LDS
     // read feeds every tile, and consecutive MFMAs go to different accumulators
-    sfor<2>([&](auto nn) {
+    if constexpr (!P0) sfor<2>([&](auto nn) {
       constexpr int net = decltype(nn)::value;
       if constexpr (M::owns_f(W, d, net)) {
         constexpr int KP = M::kin(net, d);

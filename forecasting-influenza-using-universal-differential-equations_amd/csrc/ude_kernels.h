@@ -314,9 +314,17 @@ __device__ __forceinline__ void load_x_frags(Rsrc rs, int lane, f4* fx) {
 // Layer 0 of a record with at most 4 dynamic features (R = 1: S, I, R) and the static ones hoisted: every
 // K step but the first multiplies padding, so the phase runs ONE MFMA per output tile with lane (o, g)
 // holding W[o][g] and feature g instead of KP / 4 -- the same non-zero products added in the same order
-// (the padded steps add exact zeros), so bitwise the same layer output.
+// (the padded steps add exact zeros), so bitwise the same layer output.  With packo below: M1 FaFp step
+// 7.50 -> 7.34 ms, gradients bitwise equal; Fp [32, 32] 3.15 -> 3.17 ms (profiles/r06/ab_pack_r1/).
 template <class M>
 constexpr bool pack0() { return M::HOIST && M::F <= 4 && M::F16 == 16; }
+// The same for the input gradient of an output layer with at most 4 outputs (R = 1: the 2 rates, the 3
+// Fa components): K = the 16-padded outputs, one MFMA per input tile with lane (h, g) holding W[g][h]
+// and dZ[g] (register-resident weights only: the packed values are formed once per launch).
+template <class M>
+constexpr bool packo(int net, int d) {
+  return M::has(net, d) && d > 0 && d == M::nl(net) - 1 && M::kout(net, d) == 16 && M::out_dim(net, d) <= 4;
+}
 
 // Register-resident weights (Model::WREG): every fragment / bias quad wave W reads in the
 // forward (and, BWD, the input-gradient fragments), loaded once per launch.
@@ -331,8 +339,20 @@ struct WRegs {
   static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
   static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
   static constexpr int NP0 = (ON && NEED_F && pack0<M>()) ? M::NZ(W) : 0;
+  // packo: the wave's output-layer input-gradient tiles in (d, m) order
+  static constexpr int po_index(int d, int m) {
+    int c = 0;
+    for (int e = 0; e < M::D; ++e)
+      for (int j = 0; j < M::XT(e); ++j) {
+        if (e == d && j == m) return c;
+        if (M::xowner(e, j) == W && packo<M>(M::xnet(e, j), e)) ++c;
+      }
+    return c;
+  }
+  static constexpr int NPO = (ON && BWD) ? po_index(M::D, 0) : 0;
   f4 wf[NF > 0 ? NF : 1], wb[NB > 0 ? NB : 1], wx[NX > 0 ? NX : 1];
   float w0[NP0 > 0 ? NP0 : 1];              // pack0: lane (o, g)'s layer-0 weight W[o][g]
+  float wo[NPO > 0 ? NPO : 1];              // packo: lane (h, g)'s output-layer weight W[g][h]
   __device__ __forceinline__ void load(Rsrc rs, int lane, bool wait = true) {
     if constexpr (ON) {
       const int g = lane >> 4;
@@ -365,6 +385,22 @@ struct WRegs {
             const float v2 = __shfl(q[2], src, 64), v3 = __shfl(q[3], src, 64);
             w0[M::nz_before(W, k)] = g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
           }
+        });
+      }
+      if constexpr (NPO > 0) {
+        sfor<M::D>([&](auto dd) {
+          constexpr int d = decltype(dd)::value;
+          if constexpr (d > 0) sfor<M::XT(d)>([&](auto mm) {
+            constexpr int m = decltype(mm)::value;
+            if constexpr (M::xowner(d, m) == W && packo<M>(M::xnet(d, m), d)) {
+              // K = 16 outputs: one quad per tile, lane (h, g) holds W[4 g + e][h]
+              const f4 q = wx[M::xq_base(W, d) + M::xq_before(W, d, m)];
+              const int src = lane & 15;
+              const float v0 = __shfl(q[0], src, 64), v1 = __shfl(q[1], src, 64);
+              const float v2 = __shfl(q[2], src, 64), v3 = __shfl(q[3], src, 64);
+              wo[po_index(d, m)] = g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+            }
+          });
         });
       }
     }
@@ -1432,7 +1468,15 @@ __device__ __forceinline__ void mlp_backward(Rsrc rs, Rsrc es, float* lds, DW& d
     });
     sfor<2>([&](auto nn) {
       constexpr int net = decltype(nn)::value;
-      if constexpr (M::has(net, d) && M::owns_x(W, d, net)) {
+      if constexpr (RW && packo<M>(net, d) && M::owns_x(W, d, net)) {
+        // packo: one MFMA per tile, lane (t, g) supplies output g's gradient (padded rows are zero)
+        const float xg = rec[M::gbuf(net, d) + g];
+        sfor<M::XT(d)>([&](auto mm) {
+          constexpr int m = decltype(mm)::value;
+          if constexpr (M::xowner(d, m) == W && M::xnet(d, m) == net)
+            xa[m] = mfma4(wr.wo[WR::po_index(d, m)], xg, xa[m]);
+        });
+      } else if constexpr (M::has(net, d) && M::owns_x(W, d, net)) {
         constexpr int KP = M::kout(net, d);
         // d == 0: both nets' fragments of a tile sit back to back (P first)
         constexpr int qoff = (d == 0 && net == 1 && M::HAS_P) ? M::kout(0, 0) / 16 : 0;

@@ -78,10 +78,11 @@ class _FusedAug:
 
     Flat state [vjp_t | y (N, R, L) | a_y (N, R, L) | a_theta (params, C-ABI order)]; its derivative
     in s = -t is [-vjp_t', -f(y), a_y^T df/dy, a_y^T df/dtheta] = ude_rhs_eval_vjp with cot = a_y and
-    f scaled by -1, written into the output vector's slices by one launch (+ the deterministic
-    gradient reductions).  ``comb`` / ``ratio`` are the controller's dense passes (eager_dopri5's
-    ``vec``): ude_lincomb, and the mixed error norm with the y / a_y pieces' sums of squares from
-    ude_scaled_sumsq (the parameter pieces are small and stay PyTorch)."""
+    f scaled by -1, written into the output vector's slices by one call (the evaluation + VJP kernel and
+    one tail launch).  ``comb_hc`` / ``ratio_dt`` serve adaptive.host_scalar_dopri5 (coefficients by
+    value, ude_lincomb_hc; the error ratio and next step size from ude_dopri_ratio over the y / a_y pieces'
+    ude_scaled_sumsq sums, the parameter pieces' RMS in PyTorch for the mixed norm); ``comb`` / ``ratio``
+    are the same passes behind eager_dopri5's ``vec`` interface."""
 
     def __init__(self, func, y: torch.Tensor, adjoint_params, seminorm: bool):
         from . import eval_rhs
@@ -125,6 +126,8 @@ class _FusedAug:
                               -1.0, ob + 4 * (1 + n), self.ws.data_ptr(), ob + 4 * (1 + 2 * n), self.stream)
         return out
 
+    # comb / ratio: eager_dopri5's ``vec`` interface (device-scalar coefficients, PyTorch ratio) -- the
+    # operator chain host_scalar_dopri5 is checked against bit for bit (tests/test_adjoint.py)
     def comb(self, base, ks, c) -> torch.Tensor:
         out = torch.empty_like(ks[0])
         c = c.to(torch.float32).contiguous()

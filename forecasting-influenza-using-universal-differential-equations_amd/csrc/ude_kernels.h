@@ -315,9 +315,13 @@ __device__ __forceinline__ void load_x_frags(Rsrc rs, int lane, f4* fx) {
 // K step but the first multiplies padding, so the phase runs ONE MFMA per output tile with lane (o, g)
 // holding W[o][g] and feature g instead of KP / 4 -- the same non-zero products added in the same order
 // (the padded steps add exact zeros), so bitwise the same layer output.  With packo below: M1 FaFp step
-// 7.50 -> 7.34 ms, gradients bitwise equal; Fp [32, 32] 3.15 -> 3.17 ms (profiles/r06/ab_pack_r1/).
+// 7.50 -> 7.34 ms, gradients bitwise equal (profiles/r06/ab_pack_r1/).
 template <class M>
 constexpr bool pack0() { return M::HOIST && M::F <= 4 && M::F16 == 16; }
+// ... for the waves that own at least two layer-0 tiles: with one tile per wave (Fp [32, 32]) the packed
+// phase measured 1% slower (fwd 1.507 -> 1.522 ms, profiles/r06/ab_pack_r1/ab_fp32_4way.txt)
+template <class M, int W>
+constexpr bool pack0_w() { return pack0<M>() && M::NZ(W) >= 2; }
 // The same for the input gradient of an output layer with at most 4 outputs (R = 1: the 2 rates, the 3
 // Fa components): K = the 16-padded outputs, one MFMA per input tile with lane (h, g) holding W[g][h]
 // and dZ[g] (register-resident weights only: the packed values are formed once per launch).
@@ -338,7 +342,7 @@ struct WRegs {
   static constexpr bool NEED_F = NEED_F_;   // a stored-activation RK4 backward never runs the forward
   static constexpr int NF = (ON && NEED_F) ? M::WF_Q(W) : 0, NB = (ON && NEED_F) ? M::WB_Q(W) : 0;
   static constexpr int NX = (ON && BWD) ? M::WX_Q(W) : 0;
-  static constexpr int NP0 = (ON && NEED_F && pack0<M>()) ? M::NZ(W) : 0;
+  static constexpr int NP0 = (ON && NEED_F && pack0_w<M, W>()) ? M::NZ(W) : 0;
   // packo: the wave's output-layer input-gradient tiles in (d, m) order
   static constexpr int po_index(int d, int m) {
     int c = 0;
@@ -430,7 +434,7 @@ __device__ __forceinline__ void mlp_forward(Rsrc rs, float* lds, const f4* c1, i
     // before its first MFMA -- unless they would not fit next to the working set (the Bayesian
     // state model's layer 0, K = 416: 208 VGPRs, spilled at the forward's 256): then chunk by chunk
     constexpr bool CHUNK_A = !RW && NF > 24;
-    constexpr bool P0 = d == 0 && pack0<M>();
+    constexpr bool P0 = d == 0 && pack0_w<M, W>();
     f4 fr[(NF > 0 && !RW && !CHUNK_A) ? NF : 1], bias[(M::FT(d) > 0 && !RW) ? M::FT(d) : 1];
     float w0s[(P0 && !RW && M::NZ(W) > 0) ? M::NZ(W) : 1];
     if constexpr (!RW) {

@@ -3180,7 +3180,7 @@ __device__ void static_grad_chunk(const float* __restrict__ g0buf, const float* 
   f4 acc[NOT];
 #pragma unroll
   for (int o = 0; o < NOT; ++o) acc[o] = f4zero();
-  #pragma unroll 2
+  #pragma unroll 4
   for (int tile = tb + w; tile < te; tile += WAVES) {
     f4 a[NOT];
 #pragma unroll

@@ -171,6 +171,68 @@ def test_vector_pass_controller_matches_operator_chain(pkg):
     assert normwise_rel(rb, ra) < 1e-13
 
 
+def test_host_scalar_controller_matches_eager_cpu(pkg):
+    """adaptive.host_scalar_dopri5 (odeint_adjoint's fused backward) against eager_dopri5 with the
+    same vector passes, on CPU in fp32: host-mirrored step ends / sizes and fp32 coefficient products,
+    the same attempts, bitwise the same outputs (several output times, so several dense outputs); the
+    ratio / step-size callback restates ude_dopri_ratio with PyTorch operators, as vec.ratio + the
+    eager update form them.  Plus the controller's assertions."""
+    from ude_amd.adaptive import eager_dopri5, host_scalar_dopri5, MAX_NUM_STEPS
+    A = torch.tensor([[-0.5, 1.0, 0.0], [-1.0, -0.5, 0.2], [0.0, 0.3, -0.1]])
+    atol, rtol = 1e-7, 1e-5
+
+    class Vec:
+        @staticmethod
+        def comb(base, ks, c):
+            acc = ks[0] * c[0]
+            for j in range(1, len(ks)):
+                acc = acc + ks[j] * c[j]
+            return acc if base is None else base + acc
+
+        @staticmethod
+        def ratio(err, y, y1):
+            return (err / (atol + rtol * torch.max(y.abs(), y1.abs()))).pow(2).mean().sqrt().double()
+
+    class HV:
+        @staticmethod
+        def comb_hc(base, ks, coef):
+            return Vec.comb(base, ks, torch.tensor([float(c) for c in coef], dtype=torch.float32))
+
+        @staticmethod
+        def ratio_dt(err, y, y1, dt, nonfinite):
+            r = Vec.ratio(err, y, y1)
+            rf = float(r)
+            if rf == 0:
+                dtn = torch.tensor(dt, dtype=torch.float64) * 10.0
+            else:
+                fac = torch.clamp(0.9 / r.to(torch.float64) ** 0.2, min=1.0 if rf < 1 else 0.2, max=10.0)
+                dtn = torch.tensor(dt, dtype=torch.float64) * fac
+            return rf, float(dtn), bool(nonfinite)
+
+    calls = {"a": 0, "b": 0}
+
+    def fa(tt, y):
+        calls["a"] += 1
+        return y @ A.T
+
+    def fb(tt, y):
+        calls["b"] += 1
+        return y @ A.T
+    y0 = torch.tensor([[1.0, 0.5, -0.3], [0.2, -0.1, 0.7]])
+    t = torch.tensor([0.0, 0.37, 1.1, 2.9, 3.0], dtype=torch.float64)
+    ra = eager_dopri5(fa, y0, t, rtol, atol, None, MAX_NUM_STEPS, norm=None, vec=Vec)
+    rb = host_scalar_dopri5(fb, y0, t, rtol, atol, None, MAX_NUM_STEPS,
+                            lambda v: v.abs().pow(2).mean().sqrt(), HV)
+    assert calls["a"] == calls["b"] > 20
+    assert torch.equal(ra, rb)
+    with pytest.raises(AssertionError, match="underflow in dt"):
+        host_scalar_dopri5(fb, y0, t + 1.0, rtol, atol, 1e-300, MAX_NUM_STEPS, None, HV)
+    with pytest.raises(AssertionError, match="non-finite values in state"):
+        host_scalar_dopri5(fb, y0 * float("inf"), t, rtol, atol, 0.1, MAX_NUM_STEPS, None, HV)
+    with pytest.raises(AssertionError, match="max_num_steps exceeded"):
+        host_scalar_dopri5(fb, y0, t, rtol, atol, None, 2, lambda v: v.abs().pow(2).mean().sqrt(), HV)
+
+
 def test_eager_product_is_differentiable(pkg):
     mod = _module(pkg, "Fp", 1, [32, 32], None)
     y0 = _y0(8, 1).requires_grad_(True)
